@@ -1,0 +1,84 @@
+# QuEST for MI355X - build of the native libraries.
+#
+#   make            -> CPU (host) libraries, fp64 + fp32   (no GPU needed)
+#   make hip        -> HIP libraries for gfx950, fp64 + fp32 (hipcc cross-compiles)
+#   make all        -> both
+#   make examples   -> C examples linked against the fp64 libraries
+#
+# Outputs go to quest_amd/lib/ so they travel with the repository snapshot:
+#   libQuEST_cpu_f64.so  libQuEST_cpu_f32.so  libQuEST_hip_f64.so  libQuEST_hip_f32.so
+# plus libQuEST.so -> libQuEST_hip_f64.so for C programs (-lQuEST).
+
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       ?= g++
+ARCH      ?= gfx950
+BUILD     := build
+LIBDIR    := quest_amd/lib
+JOBS      ?= 8
+
+COMMON_SRC := src/api/api.cpp src/api/validation.cpp src/api/qasm.cpp src/api/common.cpp \
+              src/api/mt19937.cpp src/core/router.cpp src/core/tiles.cpp src/comm/bootstrap.cpp
+CPU_SRC    := $(COMMON_SRC) src/comm/comm_socket.cpp src/cpu/backend_cpu.cpp
+HIP_HOST   := $(COMMON_SRC) src/comm/comm_rccl.cpp
+HIP_DEV    := src/hip/backend_hip.hip src/hip/kernels_gates.hip src/hip/kernels_reduce.hip src/hip/kernels_misc.hip
+
+INCLUDES   := -Iinclude -Isrc
+CXXFLAGS   := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $(INCLUDES)
+HIPFLAGS   := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-function \
+              -Wno-unused-result -munsafe-fp-atomics $(INCLUDES) -D__HIP_ROCclr__
+HIPHOST    := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Wno-unused-result $(INCLUDES) -I$(ROCM)/include
+
+.PHONY: cpu hip all clean examples
+
+cpu: $(LIBDIR)/libQuEST_cpu_f64.so $(LIBDIR)/libQuEST_cpu_f32.so
+hip: $(LIBDIR)/libQuEST_hip_f64.so $(LIBDIR)/libQuEST_hip_f32.so $(LIBDIR)/libQuEST.so
+all: cpu hip
+
+# ---------------------------------------------------------------- CPU build
+define cpu_rules
+$(BUILD)/cpu_f$(2)/%.o: %.cpp $(wildcard include/*.h src/*/*.hpp)
+	@mkdir -p $$(dir $$@)
+	$(CXX) $(CXXFLAGS) -DQuEST_PREC=$(1) -c $$< -o $$@
+
+$(LIBDIR)/libQuEST_cpu_f$(2).so: $(patsubst %.cpp,$(BUILD)/cpu_f$(2)/%.o,$(CPU_SRC))
+	@mkdir -p $(LIBDIR)
+	$(CXX) -shared -o $$@ $$^ -lpthread
+endef
+$(eval $(call cpu_rules,2,64))
+$(eval $(call cpu_rules,1,32))
+
+# ---------------------------------------------------------------- HIP build
+define hip_rules
+$(BUILD)/hip_f$(2)/%.o: %.cpp $(wildcard include/*.h src/*/*.hpp)
+	@mkdir -p $$(dir $$@)
+	$(HIPCC) $(HIPHOST) -DQuEST_PREC=$(1) -c $$< -o $$@
+
+$(BUILD)/hip_f$(2)/%.o: %.hip $(wildcard include/*.h src/*/*.hpp src/hip/*.h)
+	@mkdir -p $$(dir $$@)
+	$(HIPCC) $(HIPFLAGS) -DQuEST_PREC=$(1) -c $$< -o $$@
+
+$(LIBDIR)/libQuEST_hip_f$(2).so: $(patsubst %.cpp,$(BUILD)/hip_f$(2)/%.o,$(HIP_HOST)) $(patsubst %.hip,$(BUILD)/hip_f$(2)/%.o,$(HIP_DEV))
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $$@ $$^ -ldl -lpthread
+endef
+$(eval $(call hip_rules,2,64))
+$(eval $(call hip_rules,1,32))
+
+$(LIBDIR)/libQuEST.so: $(LIBDIR)/libQuEST_hip_f64.so
+	ln -sf libQuEST_hip_f64.so $@
+
+# ---------------------------------------------------------------- examples
+EXAMPLES := tutorial_example damping_example bernstein_vazirani_circuit random_circuit_benchmark
+examples: $(addprefix $(BUILD)/examples/,$(addsuffix _cpu,$(EXAMPLES)))
+
+$(BUILD)/examples/%_cpu: examples/%.c $(LIBDIR)/libQuEST_cpu_f64.so
+	@mkdir -p $(dir $@)
+	gcc -O2 -std=c99 -Iinclude $< -o $@ -L$(LIBDIR) -lQuEST_cpu_f64 -Wl,-rpath,$(abspath $(LIBDIR)) -lm
+
+$(BUILD)/examples/%_hip: examples/%.c $(LIBDIR)/libQuEST_hip_f64.so
+	@mkdir -p $(dir $@)
+	gcc -O2 -std=c99 -Iinclude $< -o $@ -L$(LIBDIR) -lQuEST_hip_f64 -Wl,-rpath,$(abspath $(LIBDIR)) -lm
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR)/*.so

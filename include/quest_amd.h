@@ -1,0 +1,73 @@
+/* MI355X-native extensions to the QuEST API.
+ *
+ * Everything in QuEST.h behaves as in the reference.  These functions expose
+ * what the MI355X design adds: deferred, fused gate execution; explicit
+ * flush/sync; runtime statistics; host mirrors and zero-copy device access
+ * for interop (e.g. with PyTorch); and error handling without exit().
+ */
+#ifndef QUEST_AMD_H
+#define QUEST_AMD_H
+
+#include "QuEST.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Called instead of exit() on invalid input; the API call then returns
+ * without modifying any state.  Pass NULL to restore print-and-exit. */
+typedef void (*QuESTErrorHandler)(int errorCode, const char* message, const char* function);
+void setQuESTErrorHandler(QuESTErrorHandler handler);
+
+/* Gate fusion: unitaries are queued per register and applied in as few
+ * passes over the state as possible (LDS-tiled passes on the GPU).  Any
+ * operation that reads the state flushes the queue first, so results are
+ * identical with fusion on or off.  Default: on (env QUEST_FUSION=0: off). */
+void setGateFusion(int enabled);
+int getGateFusion(void);
+/* Maximum number of qubits spanned by one fused pass (0 = default). */
+void setFusionMaxQubits(int numQubits);
+
+/* Submit every queued operation of the register to the device (async). */
+void flushQureg(Qureg qureg);
+/* flushQureg + wait for the device. */
+void syncQureg(Qureg qureg);
+
+/* Host mirror (Qureg.stateVec), allocated only when QUEST_HOST_MIRROR=1 at
+ * createQureg time on the HIP build. */
+void copyStateToGPU(Qureg qureg);
+void copyStateFromGPU(Qureg qureg);
+
+/* Copy this rank's chunk to / from caller-owned buffers that live where the
+ * state lives (device memory on the HIP build).  Register must be in the
+ * canonical qubit layout (it is made canonical first). */
+void copyChunkToBuffers(Qureg qureg, qreal* re, qreal* im);
+void copyChunkFromBuffers(Qureg qureg, const qreal* re, const qreal* im);
+
+/* Restore the canonical qubit layout after distributed qubit remapping. */
+void canonicaliseQureg(Qureg qureg);
+/* physical bit position of each logical qubit of the state-vector */
+void getQubitLayout(Qureg qureg, int* physicalOfLogical);
+
+typedef struct QuESTStats {
+    long long opsQueued;      /* elementary ops accepted by the backend */
+    long long passes;         /* passes over the state (kernel launches of gate kernels) */
+    long long fusedOps;       /* ops applied inside multi-op passes */
+    long long swaps;          /* global<->local qubit swaps (distributed) */
+    long long bytesExchanged; /* bytes sent to other ranks */
+    long long reductions;     /* reduction kernels */
+} QuESTStats;
+void getQuESTStats(QuESTStats* stats);
+void resetQuESTStats(void);
+
+/* Name of the compiled backend: "HIP" (gfx950) or "CPU". */
+const char* getQuESTBackend(void);
+
+/* Seed array used by seedQuESTDefault on this rank (after broadcast). */
+void getQuESTSeeds(unsigned long* seeds, int* numSeeds);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QUEST_AMD_H */

@@ -1,0 +1,161 @@
+// TCP star rendezvous used once at createQuESTEnv() time to exchange the RCCL
+// unique id (HIP build) or the socket-mesh endpoints (CPU build).
+// The reference bootstraps with MPI_Init (QuEST_cpu_distributed.c:135-164);
+// MPI is not part of this stack, so the rendezvous is a few hundred bytes
+// over one TCP listener on rank 0.
+#include "comm.hpp"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace qa {
+namespace boot {
+
+static std::string envOr(const char* a, const char* b, const char* dflt) {
+    if (const char* v = getenv(a)) return v;
+    if (b)
+        if (const char* v = getenv(b)) return v;
+    return dflt;
+}
+
+static int bootstrapPort() {
+    if (const char* p = getenv("QUEST_BOOTSTRAP_PORT")) return atoi(p);
+    if (const char* p = getenv("MASTER_PORT")) return atoi(p) + 1;
+    return 29517;
+}
+
+static void fatal(const char* what) {
+    fprintf(stderr, "QuEST bootstrap error: %s\n", what);
+    exit(EXIT_FAILURE);
+}
+
+static void writeAll(int fd, const void* buf, size_t n) {
+    const char* p = (const char*)buf;
+    while (n) {
+        ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+        if (k <= 0) fatal("send failed");
+        p += k;
+        n -= (size_t)k;
+    }
+}
+
+static void readAll(int fd, void* buf, size_t n) {
+    char* p = (char*)buf;
+    while (n) {
+        ssize_t k = ::recv(fd, p, n, 0);
+        if (k <= 0) fatal("recv failed");
+        p += k;
+        n -= (size_t)k;
+    }
+}
+
+static double timeoutSeconds() {
+    if (const char* t = getenv("QUEST_BOOTSTRAP_TIMEOUT")) return atof(t);
+    return 300.0;
+}
+
+std::string hostAddress() {
+    return envOr("QUEST_BOOTSTRAP_ADDR", "MASTER_ADDR", "127.0.0.1");
+}
+
+void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
+    char* out = (char*)all;
+    memcpy(out + (size_t)rank * bytes, mine, bytes);
+    if (size == 1) return;
+
+    const std::string addr = hostAddress();
+    const int port = bootstrapPort();
+
+    if (rank == 0) {
+        int ls = socket(AF_INET, SOCK_STREAM, 0);
+        if (ls < 0) fatal("socket");
+        int one = 1;
+        setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+        sockaddr_in sa{};
+        sa.sin_family = AF_INET;
+        sa.sin_port = htons((uint16_t)port);
+        sa.sin_addr.s_addr = htonl(INADDR_ANY);
+        if (bind(ls, (sockaddr*)&sa, sizeof sa) != 0) fatal("bind (is QUEST_BOOTSTRAP_PORT free?)");
+        if (listen(ls, size) != 0) fatal("listen");
+        std::vector<int> fds(size, -1);
+        for (int k = 1; k < size; k++) {
+            int fd = accept(ls, nullptr, nullptr);
+            if (fd < 0) fatal("accept");
+            int r = -1;
+            readAll(fd, &r, sizeof r);
+            if (r <= 0 || r >= size || fds[r] >= 0) fatal("bad rank in bootstrap");
+            readAll(fd, out + (size_t)r * bytes, bytes);
+            fds[r] = fd;
+        }
+        for (int r = 1; r < size; r++) {
+            writeAll(fds[r], out, bytes * (size_t)size);
+            close(fds[r]);
+        }
+        close(ls);
+        return;
+    }
+
+    // non-root: connect with retries until rank 0 listens
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(addr.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res)
+        fatal("cannot resolve bootstrap address");
+    auto t0 = std::chrono::steady_clock::now();
+    int fd = -1;
+    while (true) {
+        fd = socket(AF_INET, SOCK_STREAM, 0);
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+        close(fd);
+        double waited =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (waited > timeoutSeconds()) fatal("timed out connecting to rank 0");
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+    freeaddrinfo(res);
+    writeAll(fd, &rank, sizeof rank);
+    writeAll(fd, mine, bytes);
+    readAll(fd, out, bytes * (size_t)size);
+    close(fd);
+}
+
+}  // namespace boot
+
+namespace comm {
+
+void discover(int* rank, int* size, int* localRank) {
+    auto geti = [](const char* a, const char* b, int d) {
+        if (const char* v = getenv(a)) return atoi(v);
+        if (b)
+            if (const char* v = getenv(b)) return atoi(v);
+        return d;
+    };
+    *size = geti("WORLD_SIZE", "QUEST_WORLD_SIZE", 1);
+    *rank = geti("RANK", "QUEST_RANK", 0);
+    *localRank = geti("LOCAL_RANK", "QUEST_LOCAL_RANK", *rank);
+    if (*size < 1) *size = 1;
+    if (*rank < 0 || *rank >= *size) {
+        fprintf(stderr, "QuEST: RANK=%d outside WORLD_SIZE=%d\n", *rank, *size);
+        exit(EXIT_FAILURE);
+    }
+    if (*size & (*size - 1)) {
+        fprintf(stderr, "QuEST: WORLD_SIZE=%d must be a power of 2\n", *size);
+        exit(EXIT_FAILURE);
+    }
+}
+
+}  // namespace comm
+}  // namespace qa

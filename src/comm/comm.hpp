@@ -1,0 +1,53 @@
+// Inter-rank communication used by the distributed router (src/core/router.cpp).
+//
+// Replaces the reference's MPI layer (QuEST/src/CPU/QuEST_cpu_distributed.c,
+// call sites listed in SURVEY.md §2.5).  One process per GPU; the transport is
+// chosen at compile time with the backend:
+//   HIP build  -> RCCL (comm_rccl.cpp): pairwise ncclSend/ncclRecv over the
+//                 direct xGMI link, ncclAllReduce / ncclBroadcast, all ordered
+//                 on the backend's HIP stream (no host round trip per slice);
+//   CPU build  -> TCP sockets (comm_socket.cpp), used for multi-process tests.
+// Both are bootstrapped by bootstrap.cpp from torchrun-style environment
+// variables (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT) or
+// QUEST_BOOTSTRAP_ADDR / QUEST_BOOTSTRAP_PORT.
+#pragma once
+
+#include <cstddef>
+#include <string>
+
+namespace qa {
+namespace comm {
+
+// Rank / world discovered from the environment (1 rank when unset).
+void discover(int* rank, int* size, int* localRank);
+
+void init(int rank, int size);
+void finalize();
+bool active();  // true when size > 1
+
+// Exchange `bytes` with `peer`: send from `send`, receive into `recv`
+// (both backend comm buffers; must not overlap).
+void sendrecv(int peer, const void* send, void* recv, size_t bytes);
+// In-place sum of host doubles across ranks.
+void allreduceSum(double* vals, int n);
+// In-place logical AND of a host int across ranks.
+int allreduceAnd(int v);
+// Broadcast host bytes from root.
+void bcastHost(void* buf, size_t bytes, int root);
+// Gather `bytesPerRank` from every rank into recv (rank order); comm buffers.
+void allgather(const void* send, void* recv, size_t bytesPerRank);
+void barrier();
+std::string describe();
+
+}  // namespace comm
+
+// ---- bootstrap (bootstrap.cpp) ----------------------------------------------
+namespace boot {
+// Star rendezvous through rank 0 over TCP.  Every rank contributes `bytes`;
+// every rank receives all contributions in rank order.
+void allgather(int rank, int size, const void* mine, void* all, size_t bytes);
+// Local IPv4 address string of this host, as seen by rank 0's listener.
+std::string hostAddress();
+}  // namespace boot
+
+}  // namespace qa

@@ -1,0 +1,81 @@
+// Hardware backend interface.  Exactly one implementation is linked into a
+// library build (compile-time choice, like the reference's
+// QuEST/src/CMakeLists.txt:1-15): src/hip/ (MI355X, gfx950) or src/cpu/
+// (host plumbing build used on machines without a GPU and as the oracle).
+//
+// Every function acts on THIS rank's chunk only; all index arguments are
+// physical and chunk-local unless stated otherwise.  Reductions return this
+// chunk's partial sums (fp64 accumulation); the router combines ranks.
+#pragma once
+
+#include "core.hpp"
+
+namespace qa {
+namespace be {
+
+// ---- environment -------------------------------------------------------
+void envInit(int rank, int numRanks, int localRank);
+void envFinalize();
+void deviceSync();                 // wait for all queued device work
+std::string describe();            // device/backend description for reports
+const char* shortName();           // "HIP" or "CPU"
+bool stateOnHost();                // CPU build: amplitudes are host memory
+
+// ---- memory --------------------------------------------------------------
+void allocState(QuregImpl& q);     // sets q.re / q.im (numAmpsPerChunk each)
+void freeState(QuregImpl& q);
+void* allocComm(size_t bytes);     // buffer usable by the comm transport
+void freeComm(void* p);
+
+// ---- gate queue ----------------------------------------------------------
+// Ops are queued per register and applied, possibly fused, at the latest
+// when flush() is called.  Every other backend function flushes first.
+void enqueue(QuregImpl& q, const Op& op);
+void flush(QuregImpl& q);
+
+// ---- state initialisation -------------------------------------------------
+void fill(QuregImpl& q, real re, real im);                     // every amp
+void setAmp(QuregImpl& q, i64 local, real re, real im);        // one amp
+void initDebug(QuregImpl& q, i64 globalOffset);                // amp[g] = (2g + i(2g+1))/10
+// amplitudes whose physical bit `bit` equals `outcome` := val, others 0
+void fillWhereBit(QuregImpl& q, int bit, int outcome, real val);
+void writeAmps(QuregImpl& q, i64 local, const real* re, const real* im, i64 n);   // host -> chunk
+void readAmps(QuregImpl& q, i64 local, real* re, real* im, i64 n);                // chunk -> host
+void copyState(QuregImpl& dst, QuregImpl& src);
+
+// ---- reductions (partials of this chunk) -----------------------------------
+// sum |amp|^2 over amplitudes whose physical bit `bit` == bitVal (bit < 0: all)
+double sumSq(QuregImpl& q, int bit, int bitVal);
+// sum conj(bra) * ket
+void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]);
+// Density-matrix diagonal: sum over logical row r in [0, 2^n) of Re rho(r,r),
+// restricted to r with logical bit `skipBit` == 0 when skipBit >= 0.  The
+// physical flat index of rho(r,r) is sum_{j : bit j of r} offs[j]; only
+// indices inside [chunkStart, chunkStart + numAmpsPerChunk) contribute.
+double densDiagSum(QuregImpl& q, const u64* offs, int n, int skipBit, i64 chunkStart);
+
+// ---- non-unitary local ops --------------------------------------------------
+// a := alpha a + beta b
+void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta);
+// density matrix from a full pure state held in a comm buffer (2^n amps):
+// element at chunk-local k (global g = chunkStart + k, r = g mod 2^n,
+// c = g div 2^n) := psi_r conj(psi_c)
+void densInitPure(QuregImpl& rho, const real* psiRe, const real* psiIm, int n, i64 chunkStart);
+// sum_{r,c in chunk} Re[conj(psi_r) rho(r,c) psi_c]
+double densFidelity(QuregImpl& rho, const real* psiRe, const real* psiIm, int n, i64 chunkStart);
+
+// ---- distributed support -----------------------------------------------------
+// Gather / scatter the amplitudes whose local bit `bit` == bitVal, in
+// increasing index order, items [start, start+count) of that sub-sequence.
+void packBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, real* bufRe, real* bufIm);
+void unpackBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, const real* bufRe,
+               const real* bufIm);
+// chunk amplitudes [local, local+n) -> comm buffer / comm buffer -> chunk
+void toBuffer(QuregImpl& q, i64 local, i64 n, real* bufRe, real* bufIm);
+void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* bufRe, const real* bufIm);
+// host <-> comm buffer
+void bufferToHost(const real* buf, real* host, i64 n);
+void hostToBuffer(const real* host, real* buf, i64 n);
+
+}  // namespace be
+}  // namespace qa

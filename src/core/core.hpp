@@ -1,0 +1,102 @@
+// Internal core types shared by the API front-end, the distributed router, the
+// fusion planner and the two compile-time backends (HIP for gfx950, host C++).
+//
+// Design (see docs/ARCHITECTURE.md):
+//   API (logical qubits)  ->  router (logical->physical map, RCCL swaps,
+//   chunk predicates)  ->  backend queue (physical local ops, fused into LDS
+//   tile passes on the GPU)  ->  kernels.
+//
+// The reference's equivalent boundary is QuEST/src/QuEST_internal.h:22-188
+// (statevec_* / densmatr_* per backend); here the backend surface is much
+// smaller because every unitary reduces to four op kinds (Op below).
+#pragma once
+
+#include "QuEST.h"
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace qa {
+
+using real = qreal;
+using i64 = long long;
+using u64 = unsigned long long;
+
+struct cplx {
+    real re, im;
+};
+
+inline cplx cmul(cplx a, cplx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+inline cplx cadd(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
+inline cplx cconj(cplx a) { return {a.re, -a.im}; }
+
+// Elementary operation on this rank's chunk, in PHYSICAL LOCAL qubit positions.
+enum class OpKind : int {
+    Mat2 = 0,       // 2x2 complex matrix on t[0]; amplitudes whose ctrl bits are all 1
+    Diag = 1,       // multiply amplitudes with (index & ctrl) == ctrl by m[0]
+    Mat4 = 2,       // 4x4 complex on (t[0], t[1]); group index = bit(t0) + 2 bit(t1)
+    DensChan2 = 3,  // two-qubit dephase/depolarise superoperator, see below
+};
+
+// DensChan2 acts on the 16 elements spanned by t = {row q1, row q2, col q1, col q2}.
+// With a = bit(t0) + 2 bit(t1) and b = bit(t2) + 2 bit(t3):
+//   a != b : x *= m[0].re                          (off-diagonal dephasing)
+//   a == b : x_aa = m[1].re x_aa + m[2].re/4 * sum_a' x_a'a'  (depolarising mix)
+struct Op {
+    OpKind kind = OpKind::Mat2;
+    int nt = 1;          // number of valid targets in t[]
+    int t[4] = {0, 0, 0, 0};
+    u64 ctrl = 0;        // local control mask (Diag: the phase mask)
+    cplx m[16];          // row-major matrix / parameters
+};
+
+// Library-side state of a register.  Qureg.qasmLog points at `log`, which is
+// the first member, so the impl is recovered from any Qureg passed by value
+// without changing the reference's struct layout.
+struct QuregImpl {
+    QASMLogger log;
+    unsigned magic;
+    bool isDensity;
+    int nRep;            // qubits represented
+    int nSV;             // qubits in the state-vector (2 nRep for density)
+    int L;               // physical qubits held locally (nSV - log2 numChunks)
+    i64 numAmpsPerChunk;
+    i64 numAmpsTotal;
+    int chunkId;
+    int numChunks;
+    real* re;            // this chunk's amplitudes (device memory on the HIP build)
+    real* im;
+    int l2p[64];         // logical qubit -> physical bit position
+    int p2l[64];         // physical bit position -> logical qubit
+    i64 useClock = 0;    // LRU bookkeeping for choosing swap victims
+    i64 lastUse[64];
+    std::vector<Op> pending;  // ops queued for fusion (backend-owned semantics)
+    void* be = nullptr;       // backend-private state
+    real* hostRe = nullptr;   // optional host mirror (Qureg.stateVec)
+    real* hostIm = nullptr;
+    bool permIdentity() const {
+        for (int i = 0; i < nSV; i++)
+            if (l2p[i] != i) return false;
+        return true;
+    }
+};
+
+constexpr unsigned kQuregMagic = 0x51A3D355u;
+
+QuregImpl* impl(const Qureg& q);
+
+// Global runtime state (one per process).
+struct Runtime {
+    int rank = 0;
+    int numRanks = 1;
+    int localRank = 0;
+    bool initialised = false;
+    bool fusion = true;        // QUEST_FUSION=0 disables gate fusion
+    int fuseMaxQubits = 0;     // 0 = backend default
+    i64 exchangeSliceBytes = 256ll << 20;  // QUEST_EXCHANGE_SLICE_MB
+};
+Runtime& rt();
+
+}  // namespace qa

@@ -1,0 +1,70 @@
+// Distributed router: takes operations on LOGICAL qubits from the API
+// front-end and turns them into backend ops on PHYSICAL, chunk-local qubits.
+//
+// Replaces the reference's per-gate local/remote branching
+// (QuEST/src/CPU/QuEST_cpu_distributed.c:816-1214) with one mechanism:
+//  * each register keeps a logical->physical qubit map;
+//  * a non-diagonal op whose target sits on a global (rank) bit first swaps
+//    that qubit with a local one: each rank exchanges HALF its chunk with one
+//    partner over RCCL (the reference exchanges the full chunk, per gate);
+//    the map is updated instead of swapping back, so later gates on the same
+//    qubit stay local;
+//  * controls and diagonal bits on global qubits become per-rank predicates
+//    (no communication, and a rank whose control bit is 0 does nothing);
+//  * reductions are chunk partials + one allreduce.
+#pragma once
+
+#include "core.hpp"
+
+namespace qa {
+namespace router {
+
+void create(QuregImpl& q, int nSV, bool density);
+void destroy(QuregImpl& q);
+void flush(QuregImpl& q);
+void sync(QuregImpl& q);
+
+// ---- unitary / non-unitary ops on logical qubits ----------------------------
+void mat2(QuregImpl& q, int target, const int* ctrls, int nc, const cplx m[4]);
+// amplitudes whose `qubits` are all 1 are multiplied by term
+void diag(QuregImpl& q, const int* qubits, int nq, cplx term);
+// 4x4 on (q0, q1), group index bit(q0) + 2 bit(q1)
+void mat4(QuregImpl& q, int q0, int q1, const cplx m[16]);
+void densChan2(QuregImpl& q, int r1, int r2, int c1, int c2, real offFac, real keep, real mix);
+// projective collapse of one qubit (state-vector: renorm = 1/sqrt(p))
+void collapse(QuregImpl& q, int qubit, int outcome, real renorm);
+// density matrix: keep rows and cols with the outcome, scale by 1/prob
+void densCollapse(QuregImpl& q, int qubit, int outcome, real prob);
+
+// ---- state preparation -------------------------------------------------------
+void initClassical(QuregImpl& q, i64 index);  // one amplitude = 1 (flat index)
+void initUniform(QuregImpl& q, real val);
+void initDebug(QuregImpl& q);
+void initSingleQubit(QuregImpl& q, int qubit, int outcome, real val);
+void setAmps(QuregImpl& q, i64 start, const real* re, const real* im, i64 n);
+void clone(QuregImpl& dst, QuregImpl& src);
+void densInitPure(QuregImpl& rho, QuregImpl& psi);
+void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta);
+void canonicalise(QuregImpl& q);
+
+// ---- reads and reductions (collective over ranks) -------------------------------
+cplx getAmp(QuregImpl& q, i64 flatIndex);
+double probZero(QuregImpl& q, int qubit);
+double sumSqAll(QuregImpl& q);
+double densProbZero(QuregImpl& q, int qubit);
+double densTrace(QuregImpl& q);
+cplx inner(QuregImpl& bra, QuregImpl& ket);
+double densFidelity(QuregImpl& rho, QuregImpl& psi);
+// read this rank's chunk in canonical order (host arrays of numAmpsPerChunk)
+void readChunk(QuregImpl& q, real* re, real* im);
+void writeChunk(QuregImpl& q, const real* re, const real* im);
+
+}  // namespace router
+
+// runtime statistics (quest_amd.h: QuESTStats)
+struct Stats {
+    long long opsQueued = 0, passes = 0, fusedOps = 0, swaps = 0, bytesExchanged = 0, reductions = 0;
+};
+Stats& stats();
+
+}  // namespace qa

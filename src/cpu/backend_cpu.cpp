@@ -1,0 +1,345 @@
+// Host backend: the compile-time alternative to src/hip/ for machines without
+// a GPU (the reference's QuEST_cpu_local.c role), and the
+// in-tree oracle for the HIP kernels.  Deliberately simple scalar C++: its job
+// is to execute the same tile programs (src/core/tiles.hpp) as the GPU with
+// obviously-correct loops, so every layer above the kernels (front-end,
+// router, RCCL-style swaps, fusion planner) is testable on CPU.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../core/backend.hpp"
+#include "../core/router.hpp"
+#include "../core/tiles.hpp"
+
+namespace qa {
+namespace be {
+
+namespace {
+
+inline i64 insertZero(i64 x, int bit) {
+    i64 low = x & (((i64)1 << bit) - 1);
+    return ((x >> bit) << (bit + 1)) | low;
+}
+
+void applyTileOp(const TileOp& op, int k, real* re, real* im) {
+    const unsigned n = 1u << k;
+    switch ((OpKind)op.kind) {
+        case OpKind::Mat2: {
+            const int a = op.t[0];
+            const real* m = op.m;
+            for (unsigned j = 0; j < n / 2; j++) {
+                unsigned p0 = (unsigned)insertZero(j, a), p1 = p0 | (1u << a);
+                if ((p0 & op.ctrlIn) != op.ctrlIn) continue;
+                real r0 = re[p0], i0 = im[p0], r1 = re[p1], i1 = im[p1];
+                re[p0] = m[0] * r0 - m[1] * i0 + m[2] * r1 - m[3] * i1;
+                im[p0] = m[0] * i0 + m[1] * r0 + m[2] * i1 + m[3] * r1;
+                re[p1] = m[4] * r0 - m[5] * i0 + m[6] * r1 - m[7] * i1;
+                im[p1] = m[4] * i0 + m[5] * r0 + m[6] * i1 + m[7] * r1;
+            }
+            break;
+        }
+        case OpKind::Diag: {
+            const real tr = op.m[0], ti = op.m[1];
+            for (unsigned p = 0; p < n; p++) {
+                if ((p & op.ctrlIn) != op.ctrlIn) continue;
+                real r = re[p], i = im[p];
+                re[p] = tr * r - ti * i;
+                im[p] = tr * i + ti * r;
+            }
+            break;
+        }
+        case OpKind::Mat4: {
+            const int a = op.t[0], b = op.t[1];
+            const int lo = std::min(a, b), hi = std::max(a, b);
+            for (unsigned j = 0; j < n / 4; j++) {
+                unsigned p = (unsigned)insertZero(insertZero(j, lo), hi);
+                if ((p & op.ctrlIn) != op.ctrlIn) continue;
+                unsigned idx[4];
+                real vr[4], vi[4];
+                for (int g = 0; g < 4; g++) {
+                    idx[g] = p | ((unsigned)(g & 1) << a) | ((unsigned)(g >> 1) << b);
+                    vr[g] = re[idx[g]];
+                    vi[g] = im[idx[g]];
+                }
+                for (int r = 0; r < 4; r++) {
+                    real sr = 0, si = 0;
+                    for (int c = 0; c < 4; c++) {
+                        const real mr = op.m[2 * (4 * r + c)], mi = op.m[2 * (4 * r + c) + 1];
+                        sr += mr * vr[c] - mi * vi[c];
+                        si += mr * vi[c] + mi * vr[c];
+                    }
+                    re[idx[r]] = sr;
+                    im[idx[r]] = si;
+                }
+            }
+            break;
+        }
+        case OpKind::DensChan2: {
+            int s[4] = {op.t[0], op.t[1], op.t[2], op.t[3]};
+            std::sort(s, s + 4);
+            const real off = op.m[0], keep = op.m[2], mix = op.m[4];
+            for (unsigned j = 0; j < n / 16; j++) {
+                unsigned p = (unsigned)j;
+                for (int x = 0; x < 4; x++) p = (unsigned)insertZero(p, s[x]);
+                unsigned idx[16];
+                for (int e = 0; e < 16; e++) {
+                    idx[e] = p;
+                    for (int x = 0; x < 4; x++)
+                        if ((e >> x) & 1) idx[e] |= 1u << op.t[x];
+                }
+                real sr = 0, si = 0;
+                for (int a = 0; a < 4; a++) {
+                    sr += re[idx[a + 4 * a]];
+                    si += im[idx[a + 4 * a]];
+                }
+                for (int e = 0; e < 16; e++) {
+                    int a = e & 3, b = e >> 2;
+                    if (a != b) {
+                        re[idx[e]] *= off;
+                        im[idx[e]] *= off;
+                    } else {
+                        re[idx[e]] = keep * re[idx[e]] + mix * sr / 4;
+                        im[idx[e]] = keep * im[idx[e]] + mix * si / 4;
+                    }
+                }
+            }
+            break;
+        }
+    }
+}
+
+void runProgram(QuregImpl& q, const TileProgram& prog) {
+    for (const TilePass& ps : prog.passes) {
+        const unsigned n = 1u << ps.k;
+        std::vector<i64> offs(n);
+        for (unsigned p = 0; p < n; p++) offs[p] = tileOffset(ps, p);
+        std::vector<real> br(n), bi(n);
+        const i64 tiles = (i64)1 << (q.L - ps.k);
+        for (i64 T = 0; T < tiles; T++) {
+            const i64 base = tileBase(ps, T, q.L);
+            for (unsigned p = 0; p < n; p++) {
+                br[p] = q.re[base + offs[p]];
+                bi[p] = q.im[base + offs[p]];
+            }
+            for (int o = ps.opBegin; o < ps.opEnd; o++) {
+                const TileOp& op = prog.ops[o];
+                if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
+                applyTileOp(op, ps.k, br.data(), bi.data());
+            }
+            for (unsigned p = 0; p < n; p++) {
+                q.re[base + offs[p]] = br[p];
+                q.im[base + offs[p]] = bi[p];
+            }
+        }
+        stats().passes++;
+        if (ps.opEnd - ps.opBegin > 1) stats().fusedOps += ps.opEnd - ps.opBegin;
+    }
+}
+
+int fuseQubits() {
+    int k = rt().fuseMaxQubits;
+    return k > 0 ? std::max(k, 8) : 10;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+
+void envInit(int, int, int) {}
+void envFinalize() {}
+void deviceSync() {}
+std::string describe() { return "host C++ (plumbing build, no GPU)"; }
+const char* shortName() { return "CPU"; }
+bool stateOnHost() { return true; }
+
+void allocState(QuregImpl& q) {
+    q.re = (real*)calloc((size_t)q.numAmpsPerChunk, sizeof(real));
+    q.im = (real*)calloc((size_t)q.numAmpsPerChunk, sizeof(real));
+    if (!q.re || !q.im) {
+        fprintf(stderr, "QuEST: could not allocate %lld amplitudes\n", q.numAmpsPerChunk);
+        exit(EXIT_FAILURE);
+    }
+}
+
+void freeState(QuregImpl& q) {
+    free(q.re);
+    free(q.im);
+    q.re = q.im = nullptr;
+}
+
+void* allocComm(size_t bytes) { return malloc(bytes ? bytes : 1); }
+void freeComm(void* p) { free(p); }
+
+void enqueue(QuregImpl& q, const Op& op) {
+    q.pending.push_back(op);
+    if (q.pending.size() >= 512) flush(q);
+}
+
+void flush(QuregImpl& q) {
+    if (q.pending.empty()) return;
+    TileProgram prog;
+    planTiles(q.pending, q.L, fuseQubits(), 4, rt().fusion, prog);
+    q.pending.clear();
+    runProgram(q, prog);
+}
+
+void fill(QuregImpl& q, real re, real im) {
+    flush(q);
+    for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
+        q.re[i] = re;
+        q.im[i] = im;
+    }
+}
+
+void setAmp(QuregImpl& q, i64 local, real re, real im) {
+    flush(q);
+    q.re[local] = re;
+    q.im[local] = im;
+}
+
+void initDebug(QuregImpl& q, i64 globalOffset) {
+    flush(q);
+    for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
+        i64 g = globalOffset + i;
+        q.re[i] = (real)((g * 2.0) / 10.0);
+        q.im[i] = (real)((g * 2.0 + 1.0) / 10.0);
+    }
+}
+
+void fillWhereBit(QuregImpl& q, int bit, int outcome, real val) {
+    flush(q);
+    for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
+        q.re[i] = (((i >> bit) & 1) == outcome) ? val : 0;
+        q.im[i] = 0;
+    }
+}
+
+void writeAmps(QuregImpl& q, i64 local, const real* re, const real* im, i64 n) {
+    flush(q);
+    memcpy(q.re + local, re, sizeof(real) * n);
+    memcpy(q.im + local, im, sizeof(real) * n);
+}
+
+void readAmps(QuregImpl& q, i64 local, real* re, real* im, i64 n) {
+    flush(q);
+    memcpy(re, q.re + local, sizeof(real) * n);
+    memcpy(im, q.im + local, sizeof(real) * n);
+}
+
+void copyState(QuregImpl& dst, QuregImpl& src) {
+    flush(src);
+    flush(dst);
+    memcpy(dst.re, src.re, sizeof(real) * dst.numAmpsPerChunk);
+    memcpy(dst.im, src.im, sizeof(real) * dst.numAmpsPerChunk);
+}
+
+double sumSq(QuregImpl& q, int bit, int bitVal) {
+    flush(q);
+    double s = 0;
+    for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
+        if (bit >= 0 && (int)((i >> bit) & 1) != bitVal) continue;
+        s += (double)q.re[i] * q.re[i] + (double)q.im[i] * q.im[i];
+    }
+    return s;
+}
+
+void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]) {
+    flush(bra);
+    flush(ket);
+    double r = 0, i = 0;
+    for (i64 k = 0; k < bra.numAmpsPerChunk; k++) {
+        r += (double)bra.re[k] * ket.re[k] + (double)bra.im[k] * ket.im[k];
+        i += (double)bra.re[k] * ket.im[k] - (double)bra.im[k] * ket.re[k];
+    }
+    out[0] = r;
+    out[1] = i;
+}
+
+double densDiagSum(QuregImpl& q, const u64* offs, int n, int skipBit, i64 chunkStart) {
+    flush(q);
+    double s = 0;
+    const i64 dim = (i64)1 << n;
+    for (i64 r = 0; r < dim; r++) {
+        if (skipBit >= 0 && ((r >> skipBit) & 1)) continue;
+        i64 p = 0;
+        for (int j = 0; j < n; j++)
+            if ((r >> j) & 1) p |= (i64)offs[j];
+        p -= chunkStart;
+        if (p >= 0 && p < q.numAmpsPerChunk) s += q.re[p];
+    }
+    return s;
+}
+
+void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
+    flush(a);
+    flush(b);
+    for (i64 i = 0; i < a.numAmpsPerChunk; i++) {
+        a.re[i] = alpha * a.re[i] + beta * b.re[i];
+        a.im[i] = alpha * a.im[i] + beta * b.im[i];
+    }
+}
+
+void densInitPure(QuregImpl& rho, const real* pr, const real* pi, int n, i64 chunkStart) {
+    flush(rho);
+    const i64 mask = ((i64)1 << n) - 1;
+    for (i64 k = 0; k < rho.numAmpsPerChunk; k++) {
+        i64 g = chunkStart + k, r = g & mask, c = g >> n;
+        // psi_r * conj(psi_c)
+        rho.re[k] = pr[r] * pr[c] + pi[r] * pi[c];
+        rho.im[k] = pi[r] * pr[c] - pr[r] * pi[c];
+    }
+}
+
+double densFidelity(QuregImpl& rho, const real* pr, const real* pi, int n, i64 chunkStart) {
+    flush(rho);
+    const i64 mask = ((i64)1 << n) - 1;
+    double s = 0;
+    for (i64 k = 0; k < rho.numAmpsPerChunk; k++) {
+        i64 g = chunkStart + k, r = g & mask, c = g >> n;
+        // Re[ conj(psi_r) rho psi_c ]
+        double ar = rho.re[k] * pr[c] - rho.im[k] * pi[c];
+        double ai = rho.re[k] * pi[c] + rho.im[k] * pr[c];
+        s += pr[r] * ar + pi[r] * ai;
+    }
+    return s;
+}
+
+void packBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, real* br, real* bi) {
+    flush(q);
+    for (i64 j = 0; j < count; j++) {
+        i64 i = insertZero(start + j, bit) | ((i64)bitVal << bit);
+        br[j] = q.re[i];
+        bi[j] = q.im[i];
+    }
+}
+
+void unpackBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, const real* br, const real* bi) {
+    flush(q);
+    for (i64 j = 0; j < count; j++) {
+        i64 i = insertZero(start + j, bit) | ((i64)bitVal << bit);
+        q.re[i] = br[j];
+        q.im[i] = bi[j];
+    }
+}
+
+void toBuffer(QuregImpl& q, i64 local, i64 n, real* br, real* bi) {
+    flush(q);
+    memcpy(br, q.re + local, sizeof(real) * n);
+    memcpy(bi, q.im + local, sizeof(real) * n);
+}
+
+void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* br, const real* bi) {
+    flush(q);
+    memcpy(q.re + local, br, sizeof(real) * n);
+    memcpy(q.im + local, bi, sizeof(real) * n);
+}
+
+void bufferToHost(const real* buf, real* host, i64 n) { memcpy(host, buf, sizeof(real) * n); }
+void hostToBuffer(const real* host, real* buf, i64 n) { memcpy(buf, host, sizeof(real) * n); }
+
+}  // namespace be
+}  // namespace qa
