@@ -23,11 +23,11 @@ CPU_SRC    := $(COMMON_SRC) src/comm/comm_socket.cpp src/cpu/backend_cpu.cpp
 HIP_HOST   := $(COMMON_SRC) src/comm/comm_rccl.cpp
 HIP_DEV    := src/hip/backend_hip.hip src/hip/kernels_gates.hip src/hip/kernels_reduce.hip src/hip/kernels_misc.hip
 
-INCLUDES   := -Iinclude -Isrc
+INCLUDES   := -Iinclude
 CXXFLAGS   := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $(INCLUDES)
 HIPFLAGS   := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-function \
-              -Wno-unused-result -munsafe-fp-atomics $(INCLUDES) -D__HIP_ROCclr__
-HIPHOST    := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -Wno-unused-result $(INCLUDES) -I$(ROCM)/include
+              -Wno-unused-result -munsafe-fp-atomics $(INCLUDES)
+HIPHOST    := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $(INCLUDES) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 
 .PHONY: cpu hip all clean examples
 
@@ -43,7 +43,7 @@ $(BUILD)/cpu_f$(2)/%.o: %.cpp $(wildcard include/*.h src/*/*.hpp)
 
 $(LIBDIR)/libQuEST_cpu_f$(2).so: $(patsubst %.cpp,$(BUILD)/cpu_f$(2)/%.o,$(CPU_SRC))
 	@mkdir -p $(LIBDIR)
-	$(CXX) -shared -o $$@ $$^ -lpthread
+	$(CXX) -shared -Wl,-Bsymbolic -o $$@ $$^ -lpthread
 endef
 $(eval $(call cpu_rules,2,64))
 $(eval $(call cpu_rules,1,32))
@@ -52,7 +52,7 @@ $(eval $(call cpu_rules,1,32))
 define hip_rules
 $(BUILD)/hip_f$(2)/%.o: %.cpp $(wildcard include/*.h src/*/*.hpp)
 	@mkdir -p $$(dir $$@)
-	$(HIPCC) $(HIPHOST) -DQuEST_PREC=$(1) -c $$< -o $$@
+	$(CXX) $(HIPHOST) -DQuEST_PREC=$(1) -c $$< -o $$@
 
 $(BUILD)/hip_f$(2)/%.o: %.hip $(wildcard include/*.h src/*/*.hpp src/hip/*.h)
 	@mkdir -p $$(dir $$@)
@@ -60,7 +60,7 @@ $(BUILD)/hip_f$(2)/%.o: %.hip $(wildcard include/*.h src/*/*.hpp src/hip/*.h)
 
 $(LIBDIR)/libQuEST_hip_f$(2).so: $(patsubst %.cpp,$(BUILD)/hip_f$(2)/%.o,$(HIP_HOST)) $(patsubst %.hip,$(BUILD)/hip_f$(2)/%.o,$(HIP_DEV))
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $$@ $$^ -ldl -lpthread
+	$(HIPCC) -shared -Wl,-Bsymbolic --offload-arch=$(ARCH) -o $$@ $$^ -L$(ROCM)/lib -lamdhip64 -ldl -lpthread
 endef
 $(eval $(call hip_rules,2,64))
 $(eval $(call hip_rules,1,32))

@@ -44,6 +44,11 @@ void copyStateFromGPU(Qureg qureg);
 void copyChunkToBuffers(Qureg qureg, qreal* re, qreal* im);
 void copyChunkFromBuffers(Qureg qureg, const qreal* re, const qreal* im);
 
+/* Collective read of the amplitudes [startInd, startInd + numAmps) of a
+ * state-vector (or of the flattened density matrix) into host arrays on
+ * every rank; the counterpart of setAmps. */
+void getAmps(Qureg qureg, long long int startInd, qreal* reals, qreal* imags, long long int numAmps);
+
 /* Restore the canonical qubit layout after distributed qubit remapping. */
 void canonicaliseQureg(Qureg qureg);
 /* physical bit position of each logical qubit of the state-vector */

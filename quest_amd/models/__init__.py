@@ -1,0 +1,10 @@
+"""Circuit families (see circuits.py)."""
+from .circuits import (  # noqa: F401
+    Circuit,
+    Gate,
+    bernstein_vazirani,
+    fork_benchmark,
+    ghz,
+    qft,
+    random_layered,
+)

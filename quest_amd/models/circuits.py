@@ -1,0 +1,174 @@
+"""Circuit families ("models" of this framework): a tiny gate-list IR plus
+generators for the workloads the reference ships or benchmarks.
+
+* :func:`random_layered` - depth-D random circuit: a random single-qubit gate
+  on every qubit, then a CNOT brick layer (the bench.py workload);
+* :func:`fork_benchmark` - the zhaozzz-160 fork's 30-qubit benchmark shape
+  (tutorial_example.c:29-534: 490 gates with the same gate-type histogram,
+  30 calcProbOfOutcome, 10 getAmp), regenerated with a seeded RNG;
+* :func:`qft`, :func:`ghz`, :func:`bernstein_vazirani` - the algorithms of the
+  reference's tests/algor and examples/bernstein_vazirani_circuit.c.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..utils import oracle as O
+
+ONE_QUBIT = ("h", "x", "y", "z", "s", "t", "rx", "ry", "rz")
+
+
+@dataclass
+class Gate:
+    name: str
+    qubits: tuple
+    param: float | None = None
+
+
+@dataclass
+class Circuit:
+    n: int
+    gates: list = field(default_factory=list)
+
+    def add(self, name, *qubits, param=None):
+        self.gates.append(Gate(name, tuple(int(q) for q in qubits), param))
+        return self
+
+    def __len__(self):
+        return len(self.gates)
+
+    def count(self):
+        out = {}
+        for g in self.gates:
+            out[g.name] = out.get(g.name, 0) + 1
+        return out
+
+    # -- execution ---------------------------------------------------------
+    def apply(self, reg):
+        """Apply to a quest_amd Register (one API call per gate)."""
+        for g in self.gates:
+            q = g.qubits
+            if g.param is None:
+                if g.name in ("cnot", "cy", "cz"):
+                    getattr(reg, g.name)(q[0], q[1])
+                elif g.name == "mcz":
+                    reg.mcz(list(q))
+                else:
+                    getattr(reg, g.name)(q[0])
+            else:
+                if g.name in ("crx", "cry", "crz", "cphase"):
+                    getattr(reg, g.name)(q[0], q[1], g.param)
+                else:
+                    getattr(reg, g.name)(q[0], g.param)
+
+    def apply_oracle(self, o):
+        """Apply to an oracle StateVector / DensityMatrix."""
+        mats = {"h": O.H, "x": O.X, "y": O.Y, "z": O.Z, "s": O.S, "t": O.T}
+        for g in self.gates:
+            q = g.qubits
+            if g.name in mats:
+                o.apply(mats[g.name], q[0])
+            elif g.name in ("rx", "ry", "rz"):
+                axis = {"rx": (1, 0, 0), "ry": (0, 1, 0), "rz": (0, 0, 1)}[g.name]
+                o.apply(O.rot(g.param, axis), q[0])
+            elif g.name == "phase":
+                o.apply(O.phase(g.param), q[0])
+            elif g.name in ("cnot", "cy", "cz"):
+                o.apply({"cnot": O.X, "cy": O.Y, "cz": O.Z}[g.name], q[1], [q[0]])
+            elif g.name in ("crx", "cry", "crz"):
+                axis = {"crx": (1, 0, 0), "cry": (0, 1, 0), "crz": (0, 0, 1)}[g.name]
+                o.apply(O.rot(g.param, axis), q[1], [q[0]])
+            elif g.name == "cphase":
+                o.apply(O.phase(g.param), q[1], [q[0]])
+            elif g.name == "mcz":
+                o.apply(O.Z, q[-1], list(q[:-1]))
+            else:
+                raise ValueError(g.name)
+
+    def to_qasm(self) -> str:
+        lines = ["OPENQASM 2.0;", f"qreg q[{self.n}];", f"creg c[{self.n}];"]
+        for g in self.gates:
+            args = ",".join(f"q[{q}]" for q in g.qubits)
+            name = {"cnot": "cx", "phase": "u1"}.get(g.name, g.name)
+            p = f"({g.param:.14g})" if g.param is not None else ""
+            lines.append(f"{name}{p} {args};")
+        return "\n".join(lines) + "\n"
+
+
+def random_layered(n: int, depth: int, seed: int = 0, entangle: bool = True) -> Circuit:
+    """Depth-`depth` random circuit: each layer applies a random single-qubit
+    gate (from ONE_QUBIT, random angles) to every qubit, then CNOTs on a brick
+    pattern of neighbouring pairs."""
+    rng = np.random.default_rng(seed)
+    c = Circuit(n)
+    for layer in range(depth):
+        for q in range(n):
+            name = ONE_QUBIT[rng.integers(len(ONE_QUBIT))]
+            if name in ("rx", "ry", "rz"):
+                c.add(name, q, param=float(rng.uniform(0, 2 * math.pi)))
+            else:
+                c.add(name, q)
+        if entangle:
+            for a in range(layer % 2, n - 1, 2):
+                c.add("cnot", a, a + 1)
+    return c
+
+
+_FORK_HISTOGRAM = {  # tutorial_example.c:29-518 of the fork (counted with grep)
+    "z": 44, "y": 43, "cry": 40, "cy": 40, "t": 38, "x": 37, "rx": 35, "cnot": 33,
+    "rz": 32, "crz": 32, "crx": 32, "ry": 31, "h": 28, "s": 25,
+}
+
+
+def fork_benchmark(seed: int = 2024, n: int = 30) -> Circuit:
+    """490 gates on 30 qubits with the fork benchmark's gate-type histogram,
+    in a seeded random order with random qubits and angles."""
+    rng = np.random.default_rng(seed)
+    names = [k for k, v in _FORK_HISTOGRAM.items() for _ in range(v)]
+    rng.shuffle(names)
+    c = Circuit(n)
+    for name in names:
+        if name in ("cry", "cy", "cnot", "crz", "crx"):
+            a, b = rng.permutation(n)[:2]
+            if name.startswith("cr"):
+                c.add(name, a, b, param=float(rng.uniform(0, 2 * math.pi)))
+            else:
+                c.add(name, a, b)
+        elif name in ("rx", "ry", "rz"):
+            c.add(name, rng.integers(n), param=float(rng.uniform(0, 2 * math.pi)))
+        else:
+            c.add(name, rng.integers(n))
+    return c
+
+
+def qft(n: int) -> Circuit:
+    """Quantum Fourier transform with controlled phases (no final swaps)."""
+    c = Circuit(n)
+    for j in reversed(range(n)):
+        c.add("h", j)
+        for k in reversed(range(j)):
+            c.add("cphase", k, j, param=math.pi / (1 << (j - k)))
+    return c
+
+
+def ghz(n: int) -> Circuit:
+    c = Circuit(n).add("h", 0)
+    for q in range(1, n):
+        c.add("cnot", q - 1, q)
+    return c
+
+
+def bernstein_vazirani(secret: int, n: int) -> Circuit:
+    """BV circuit on n qubits: after it, the register holds |secret>."""
+    c = Circuit(n)
+    for q in range(n):
+        c.add("h", q)
+    for q in range(n):
+        if (secret >> q) & 1:
+            c.add("z", q)
+    for q in range(n):
+        c.add("h", q)
+    return c

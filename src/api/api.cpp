@@ -916,6 +916,14 @@ void copyChunkFromBuffers(Qureg qureg, const qreal* re, const qreal* im) {
     be::deviceSync();
 }
 
+void getAmps(Qureg qureg, long long int startInd, qreal* reals, qreal* imags, long long int numAmps) {
+    if (startInd < 0 || numAmps < 0 || startInd + numAmps > qureg.numAmpsTotal) {
+        raiseError(E_INVALID_NUM_AMPS, __func__);
+        return;
+    }
+    router::readRange(Q(qureg), startInd, reals, imags, numAmps);
+}
+
 void canonicaliseQureg(Qureg qureg) { router::canonicalise(Q(qureg)); }
 
 void getQubitLayout(Qureg qureg, int* physicalOfLogical) {

@@ -1,0 +1,206 @@
+// RCCL transport (HIP build): one communicator per process / GPU, every
+// collective enqueued on the backend's HIP stream so that it is ordered after
+// the kernels that produced its input and before those that consume it.
+//
+// Pairwise exchanges (the only bulk traffic: distributed qubit swaps, see
+// src/core/router.cpp) are ncclSend + ncclRecv inside one group, i.e. both
+// directions of the single direct xGMI link between the two GPUs at once.
+// Scalars (probabilities, norms, inner products) use ncclAllReduce on a small
+// device buffer.  Replaces the reference's blocking MPI_Sendrecv /
+// MPI_Allreduce / MPI_Bcast calls (QuEST_cpu_distributed.c:41-512, 1236-1305).
+//
+// librccl is loaded with dlopen: inside a Python process that already loaded
+// PyTorch we bind to torch's RCCL (same HIP runtime); standalone C programs
+// get /opt/rocm's.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../hip/qa_hip.h"
+#include "comm.hpp"
+
+namespace qa {
+namespace comm {
+
+namespace {
+
+struct Rccl {
+    void* lib = nullptr;
+    ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*allReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*allGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*groupStart)() = nullptr;
+    ncclResult_t (*groupEnd)() = nullptr;
+    const char* (*errorString)(ncclResult_t) = nullptr;
+    ncclResult_t (*getVersion)(int*) = nullptr;
+} R;
+
+int g_rank = 0, g_size = 1;
+ncclComm_t g_comm = nullptr;
+double* g_dScalars = nullptr;   // device scratch for scalar collectives
+double* g_hScalars = nullptr;   // pinned host mirror
+std::string g_libName;
+
+void die(const char* what, ncclResult_t r) {
+    fprintf(stderr, "QuEST RCCL error (rank %d): %s: %s\n", g_rank, what, R.errorString ? R.errorString(r) : "?");
+    exit(EXIT_FAILURE);
+}
+
+#define QA_NCCL(call, what)                  \
+    do {                                     \
+        ncclResult_t _r = (call);            \
+        if (_r != ncclSuccess) die(what, _r); \
+    } while (0)
+
+template <typename F>
+void sym(F& f, const char* name) {
+    f = reinterpret_cast<F>(dlsym(R.lib, name));
+    if (!f) {
+        fprintf(stderr, "QuEST: symbol %s missing from %s\n", name, g_libName.c_str());
+        exit(EXIT_FAILURE);
+    }
+}
+
+void loadRccl() {
+    if (R.lib) return;
+    const char* env = getenv("QUEST_RCCL_LIB");
+    const char* candidates[] = {env, "librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"};
+    for (int i = 0; i < 4 && !R.lib; i++) {
+        if (!candidates[i]) continue;
+        // prefer a copy already mapped into the process (e.g. PyTorch's)
+        R.lib = dlopen(candidates[i], RTLD_NOW | RTLD_NOLOAD);
+        if (!R.lib) R.lib = dlopen(candidates[i], RTLD_NOW | RTLD_GLOBAL);
+        if (R.lib) g_libName = candidates[i];
+    }
+    if (!R.lib) {
+        fprintf(stderr, "QuEST: could not load librccl (%s)\n", dlerror());
+        exit(EXIT_FAILURE);
+    }
+    sym(R.getUniqueId, "ncclGetUniqueId");
+    sym(R.commInitRank, "ncclCommInitRank");
+    sym(R.commDestroy, "ncclCommDestroy");
+    sym(R.send, "ncclSend");
+    sym(R.recv, "ncclRecv");
+    sym(R.allReduce, "ncclAllReduce");
+    sym(R.broadcast, "ncclBroadcast");
+    sym(R.allGather, "ncclAllGather");
+    sym(R.groupStart, "ncclGroupStart");
+    sym(R.groupEnd, "ncclGroupEnd");
+    sym(R.errorString, "ncclGetErrorString");
+    sym(R.getVersion, "ncclGetVersion");
+}
+
+hipStream_t S() { return hipk::stream(); }
+
+}  // namespace
+
+void init(int rank, int size) {
+    g_rank = rank;
+    g_size = size;
+    if (size == 1) return;
+    loadRccl();
+    ncclUniqueId id;
+    memset(&id, 0, sizeof id);
+    if (rank == 0) QA_NCCL(R.getUniqueId(&id), "ncclGetUniqueId");
+    std::string all((size_t)size * sizeof id, '\0');
+    boot::allgather(rank, size, &id, &all[0], sizeof id);
+    memcpy(&id, all.data(), sizeof id);  // rank 0's id
+    QA_NCCL(R.commInitRank(&g_comm, size, id, rank), "ncclCommInitRank");
+    QA_HIP_CHECK(hipMalloc(&g_dScalars, sizeof(double) * 64));
+    QA_HIP_CHECK(hipHostMalloc(&g_hScalars, sizeof(double) * 64, hipHostMallocDefault));
+}
+
+void finalize() {
+    if (g_comm) {
+        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        R.commDestroy(g_comm);
+        g_comm = nullptr;
+        (void)hipFree(g_dScalars);
+        (void)hipHostFree(g_hScalars);
+        g_dScalars = g_hScalars = nullptr;
+    }
+    g_size = 1;
+}
+
+bool active() { return g_size > 1; }
+
+void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
+    if (peer == g_rank) {
+        QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, S()));
+        return;
+    }
+    QA_NCCL(R.groupStart(), "ncclGroupStart");
+    QA_NCCL(R.send(send, bytes, ncclUint8, peer, g_comm, S()), "ncclSend");
+    QA_NCCL(R.recv(recv, bytes, ncclUint8, peer, g_comm, S()), "ncclRecv");
+    QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+}
+
+void allreduceSum(double* vals, int n) {
+    if (g_size == 1) return;
+    for (int off = 0; off < n; off += 64) {
+        int k = n - off < 64 ? n - off : 64;
+        memcpy(g_hScalars, vals + off, sizeof(double) * k);
+        QA_HIP_CHECK(hipMemcpyAsync(g_dScalars, g_hScalars, sizeof(double) * k, hipMemcpyHostToDevice, S()));
+        QA_NCCL(R.allReduce(g_dScalars, g_dScalars, (size_t)k, ncclFloat64, ncclSum, g_comm, S()), "ncclAllReduce");
+        QA_HIP_CHECK(hipMemcpyAsync(g_hScalars, g_dScalars, sizeof(double) * k, hipMemcpyDeviceToHost, S()));
+        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        memcpy(vals + off, g_hScalars, sizeof(double) * k);
+    }
+}
+
+int allreduceAnd(int v) {
+    double d = v ? 0.0 : 1.0;
+    allreduceSum(&d, 1);
+    return d == 0.0 ? 1 : 0;
+}
+
+void bcastHost(void* buf, size_t bytes, int root) {
+    if (g_size == 1) return;
+    char* p = (char*)buf;
+    const size_t cap = sizeof(double) * 64;
+    for (size_t off = 0; off < bytes; off += cap) {
+        size_t k = bytes - off < cap ? bytes - off : cap;
+        if (g_rank == root) memcpy(g_hScalars, p + off, k);
+        QA_HIP_CHECK(hipMemcpyAsync(g_dScalars, g_hScalars, k, hipMemcpyHostToDevice, S()));
+        QA_NCCL(R.broadcast(g_dScalars, g_dScalars, k, ncclUint8, root, g_comm, S()), "ncclBroadcast");
+        QA_HIP_CHECK(hipMemcpyAsync(g_hScalars, g_dScalars, k, hipMemcpyDeviceToHost, S()));
+        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        memcpy(p + off, g_hScalars, k);
+    }
+}
+
+void allgather(const void* send, void* recv, size_t bytesPerRank) {
+    if (g_size == 1) {
+        QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytesPerRank, hipMemcpyDeviceToDevice, S()));
+        return;
+    }
+    QA_NCCL(R.allGather(send, recv, bytesPerRank, ncclUint8, g_comm, S()), "ncclAllGather");
+}
+
+void barrier() {
+    double d = 1;
+    allreduceSum(&d, 1);
+}
+
+std::string describe() {
+    if (g_size == 1) return "single process";
+    int v = 0;
+    if (R.getVersion) R.getVersion(&v);
+    char buf[256];
+    snprintf(buf, sizeof buf, "RCCL %d over xGMI (%d ranks, %s)", v, g_size, g_libName.c_str());
+    return buf;
+}
+
+}  // namespace comm
+}  // namespace qa

@@ -499,6 +499,20 @@ void readChunk(QuregImpl& q, real* re, real* im) {
     be::readAmps(q, 0, re, im, q.numAmpsPerChunk);
 }
 
+void readRange(QuregImpl& q, i64 start, real* re, real* im, i64 n) {
+    canonicalise(q);
+    for (int r = 0; r < q.numChunks; r++) {
+        i64 c0 = (i64)r * q.numAmpsPerChunk, c1 = c0 + q.numAmpsPerChunk;
+        i64 lo = std::max(start, c0), hi = std::min(start + n, c1);
+        if (lo >= hi) continue;
+        if (r == q.chunkId) be::readAmps(q, lo - c0, re + (lo - start), im + (lo - start), hi - lo);
+        if (q.numChunks > 1) {
+            comm::bcastHost(re + (lo - start), sizeof(real) * (size_t)(hi - lo), r);
+            comm::bcastHost(im + (lo - start), sizeof(real) * (size_t)(hi - lo), r);
+        }
+    }
+}
+
 void writeChunk(QuregImpl& q, const real* re, const real* im) {
     be::flush(q);
     resetLayout(q);

@@ -58,6 +58,8 @@ double densFidelity(QuregImpl& rho, QuregImpl& psi);
 // read this rank's chunk in canonical order (host arrays of numAmpsPerChunk)
 void readChunk(QuregImpl& q, real* re, real* im);
 void writeChunk(QuregImpl& q, const real* re, const real* im);
+// collective read of global amplitudes [start, start+n) onto every rank
+void readRange(QuregImpl& q, i64 start, real* re, real* im, i64 n);
 
 }  // namespace router
 

@@ -1,0 +1,294 @@
+// HIP backend for MI355X (gfx950): device/stream management, the gate queue
+// and its fused tile passes, and the thin wrappers around the kernels.
+//
+// One process per GPU.  All work of this process is issued on ONE
+// non-blocking HIP stream; RCCL exchanges are enqueued on the same stream
+// (src/comm/comm_rccl.cpp), so pack -> send/recv -> unpack needs no host
+// synchronisation.  The host blocks only when a value must come back
+// (reductions, amplitude reads) or at syncQuESTEnv.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../core/backend.hpp"
+#include "../core/router.hpp"
+#include "qa_hip.h"
+
+namespace qa {
+namespace hipk {
+
+namespace {
+hipStream_t g_stream = nullptr;
+int g_device = 0;
+int g_numCUs = 256;
+hipDeviceProp_t g_prop;
+
+// Ring of pinned upload slots for tile programs; a slot is reused only after
+// the event recorded behind its last use has completed.
+constexpr int kSlots = 32;
+constexpr size_t kSlotBytes = 128 << 10;
+char* g_progHost = nullptr;
+char* g_progDev = nullptr;
+hipEvent_t g_slotEvent[kSlots];
+bool g_slotUsed[kSlots];
+int g_nextSlot = 0;
+}  // namespace
+
+void fatal(const char* expr, const char* err, const char* file, int line) {
+    fprintf(stderr, "QuEST HIP error: %s failed: %s (%s:%d)\n", expr, err, file, line);
+    fflush(stderr);
+    exit(EXIT_FAILURE);
+}
+
+hipStream_t stream() { return g_stream; }
+int numCUs() { return g_numCUs; }
+
+}  // namespace hipk
+
+namespace be {
+
+using namespace hipk;
+
+namespace {
+
+constexpr size_t kMaxQueued = 256;
+
+int tileQubits(int L) {
+    const int cmin = sizeof(real) == 8 ? 4 : 5;
+    int kmax = rt().fuseMaxQubits > 0 ? rt().fuseMaxQubits : (sizeof(real) == 8 ? 11 : 12);
+    kmax = std::min(kmax, 13);
+    // keep at least ~128 tiles in flight for small chunks
+    int k = std::min(kmax, std::max(cmin + 4, L - 7));
+    return std::min(k, L);
+}
+
+int contiguousLow(const TilePass& ps) {
+    int c = 0;
+    while (c < ps.k && ps.pos[c] == c) c++;
+    return c;
+}
+
+void runProgram(QuregImpl& q, const TileProgram& prog) {
+    const size_t bytes = sizeof(TileOp) * prog.ops.size();
+    if (bytes > kSlotBytes) fatal("tile program", "too many ops in one flush", __FILE__, __LINE__);
+    const int s = g_nextSlot;
+    g_nextSlot = (g_nextSlot + 1) % kSlots;
+    if (g_slotUsed[s]) QA_HIP_CHECK(hipEventSynchronize(g_slotEvent[s]));
+    char* h = g_progHost + s * kSlotBytes;
+    char* d = g_progDev + s * kSlotBytes;
+    memcpy(h, prog.ops.data(), bytes);
+    QA_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, g_stream));
+    const TileOp* dOps = reinterpret_cast<const TileOp*>(d);
+    for (const TilePass& ps : prog.passes) {
+        TileArgs a;
+        a.L = q.L;
+        a.k = ps.k;
+        a.c = contiguousLow(ps);
+        a.nOps = ps.opEnd - ps.opBegin;
+        a.numTiles = 1ll << (q.L - ps.k);
+        for (int i = 0; i < 32; i++) a.pos[i] = i < ps.k ? ps.pos[i] : 0;
+        launchTilePass(q.re, q.im, a, dOps + ps.opBegin);
+        stats().passes++;
+        if (a.nOps > 1) stats().fusedOps += a.nOps;
+    }
+    QA_HIP_CHECK(hipEventRecord(g_slotEvent[s], g_stream));
+    g_slotUsed[s] = true;
+}
+
+}  // namespace
+
+void envInit(int rank, int numRanks, int localRank) {
+    (void)rank;
+    (void)numRanks;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        printf("Trying to run GPU code with no GPU available\n");
+        exit(EXIT_FAILURE);
+    }
+    g_device = localRank % count;
+    QA_HIP_CHECK(hipSetDevice(g_device));
+    QA_HIP_CHECK(hipGetDeviceProperties(&g_prop, g_device));
+    g_numCUs = g_prop.multiProcessorCount > 0 ? g_prop.multiProcessorCount : 256;
+    QA_HIP_CHECK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+    QA_HIP_CHECK(hipHostMalloc(&g_progHost, kSlots * kSlotBytes, hipHostMallocDefault));
+    QA_HIP_CHECK(hipMalloc(&g_progDev, kSlots * kSlotBytes));
+    for (int i = 0; i < kSlots; i++) {
+        QA_HIP_CHECK(hipEventCreateWithFlags(&g_slotEvent[i], hipEventDisableTiming));
+        g_slotUsed[i] = false;
+    }
+}
+
+void envFinalize() {
+    if (!g_stream) return;
+    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+    for (int i = 0; i < kSlots; i++) (void)hipEventDestroy(g_slotEvent[i]);
+    (void)hipHostFree(g_progHost);
+    (void)hipFree(g_progDev);
+    (void)hipStreamDestroy(g_stream);
+    g_stream = nullptr;
+    g_progHost = g_progDev = nullptr;
+}
+
+void deviceSync() {
+    if (g_stream) QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+}
+
+std::string describe() {
+    char buf[512];
+    snprintf(buf, sizeof buf, "%s (%s), %d CUs, %.1f GiB HBM, device %d", g_prop.name, g_prop.gcnArchName, g_numCUs,
+             (double)g_prop.totalGlobalMem / (1024.0 * 1024 * 1024), g_device);
+    return buf;
+}
+
+const char* shortName() { return "HIP"; }
+bool stateOnHost() { return false; }
+
+void allocState(QuregImpl& q) {
+    const size_t bytes = sizeof(real) * (size_t)q.numAmpsPerChunk;
+    if (hipMalloc(&q.re, bytes) != hipSuccess || hipMalloc(&q.im, bytes) != hipSuccess) {
+        fprintf(stderr, "QuEST: out of device memory allocating 2 x %.2f GiB for a %d-qubit register\n",
+                (double)bytes / (1 << 30), q.nSV);
+        exit(EXIT_FAILURE);
+    }
+}
+
+void freeState(QuregImpl& q) {
+    deviceSync();
+    (void)hipFree(q.re);
+    (void)hipFree(q.im);
+    q.re = q.im = nullptr;
+}
+
+void* allocComm(size_t bytes) {
+    void* p = nullptr;
+    QA_HIP_CHECK(hipMalloc(&p, bytes ? bytes : 16));
+    return p;
+}
+
+void freeComm(void* p) {
+    deviceSync();
+    (void)hipFree(p);
+}
+
+void enqueue(QuregImpl& q, const Op& op) {
+    q.pending.push_back(op);
+    if (q.pending.size() >= kMaxQueued) flush(q);
+}
+
+void flush(QuregImpl& q) {
+    if (q.pending.empty()) return;
+    TileProgram prog;
+    planTiles(q.pending, q.L, tileQubits(q.L), sizeof(real) == 8 ? 4 : 5, rt().fusion, prog);
+    q.pending.clear();
+    runProgram(q, prog);
+}
+
+void fill(QuregImpl& q, real re, real im) {
+    flush(q);
+    launchFill(q.re, q.im, q.numAmpsPerChunk, re, im);
+}
+
+void setAmp(QuregImpl& q, i64 local, real re, real im) {
+    flush(q);
+    launchFill(q.re + local, q.im + local, 1, re, im);
+}
+
+void initDebug(QuregImpl& q, i64 globalOffset) {
+    flush(q);
+    launchInitDebug(q.re, q.im, q.numAmpsPerChunk, globalOffset);
+}
+
+void fillWhereBit(QuregImpl& q, int bit, int outcome, real val) {
+    flush(q);
+    launchFillWhereBit(q.re, q.im, q.numAmpsPerChunk, bit, outcome, val);
+}
+
+void writeAmps(QuregImpl& q, i64 local, const real* re, const real* im, i64 n) {
+    flush(q);
+    QA_HIP_CHECK(hipMemcpyAsync(q.re + local, re, sizeof(real) * n, hipMemcpyHostToDevice, g_stream));
+    QA_HIP_CHECK(hipMemcpyAsync(q.im + local, im, sizeof(real) * n, hipMemcpyHostToDevice, g_stream));
+    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+}
+
+void readAmps(QuregImpl& q, i64 local, real* re, real* im, i64 n) {
+    flush(q);
+    QA_HIP_CHECK(hipMemcpyAsync(re, q.re + local, sizeof(real) * n, hipMemcpyDeviceToHost, g_stream));
+    QA_HIP_CHECK(hipMemcpyAsync(im, q.im + local, sizeof(real) * n, hipMemcpyDeviceToHost, g_stream));
+    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+}
+
+void copyState(QuregImpl& dst, QuregImpl& src) {
+    flush(src);
+    flush(dst);
+    const size_t bytes = sizeof(real) * (size_t)dst.numAmpsPerChunk;
+    QA_HIP_CHECK(hipMemcpyAsync(dst.re, src.re, bytes, hipMemcpyDeviceToDevice, g_stream));
+    QA_HIP_CHECK(hipMemcpyAsync(dst.im, src.im, bytes, hipMemcpyDeviceToDevice, g_stream));
+}
+
+double sumSq(QuregImpl& q, int bit, int bitVal) {
+    flush(q);
+    return reduceSumSq(q.re, q.im, q.numAmpsPerChunk, bit, bitVal);
+}
+
+void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]) {
+    flush(bra);
+    flush(ket);
+    reduceInner(bra.re, bra.im, ket.re, ket.im, bra.numAmpsPerChunk, out);
+}
+
+double densDiagSum(QuregImpl& q, const u64* offs, int n, int skipBit, i64 chunkStart) {
+    flush(q);
+    return reduceDensDiag(q.re, q.numAmpsPerChunk, offs, n, skipBit, chunkStart);
+}
+
+void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
+    flush(a);
+    flush(b);
+    launchAxpby(a.re, a.im, alpha, b.re, b.im, beta, a.numAmpsPerChunk);
+}
+
+void densInitPure(QuregImpl& rho, const real* pr, const real* pi, int n, i64 chunkStart) {
+    flush(rho);
+    launchDensInitPure(rho.re, rho.im, rho.numAmpsPerChunk, pr, pi, n, chunkStart);
+}
+
+double densFidelity(QuregImpl& rho, const real* pr, const real* pi, int n, i64 chunkStart) {
+    flush(rho);
+    return reduceDensFidelity(rho.re, rho.im, rho.numAmpsPerChunk, pr, pi, n, chunkStart);
+}
+
+void packBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, real* br, real* bi) {
+    flush(q);
+    launchPackBit(q.re, q.im, bit, bitVal, start, count, br, bi, false);
+}
+
+void unpackBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, const real* br, const real* bi) {
+    flush(q);
+    launchPackBit(q.re, q.im, bit, bitVal, start, count, const_cast<real*>(br), const_cast<real*>(bi), true);
+}
+
+void toBuffer(QuregImpl& q, i64 local, i64 n, real* br, real* bi) {
+    flush(q);
+    QA_HIP_CHECK(hipMemcpyAsync(br, q.re + local, sizeof(real) * n, hipMemcpyDeviceToDevice, g_stream));
+    QA_HIP_CHECK(hipMemcpyAsync(bi, q.im + local, sizeof(real) * n, hipMemcpyDeviceToDevice, g_stream));
+}
+
+void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* br, const real* bi) {
+    flush(q);
+    QA_HIP_CHECK(hipMemcpyAsync(q.re + local, br, sizeof(real) * n, hipMemcpyDeviceToDevice, g_stream));
+    QA_HIP_CHECK(hipMemcpyAsync(q.im + local, bi, sizeof(real) * n, hipMemcpyDeviceToDevice, g_stream));
+}
+
+void bufferToHost(const real* buf, real* host, i64 n) {
+    QA_HIP_CHECK(hipMemcpyAsync(host, buf, sizeof(real) * n, hipMemcpyDeviceToHost, g_stream));
+    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+}
+
+void hostToBuffer(const real* host, real* buf, i64 n) {
+    QA_HIP_CHECK(hipMemcpyAsync(buf, host, sizeof(real) * n, hipMemcpyHostToDevice, g_stream));
+    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+}
+
+}  // namespace be
+}  // namespace qa

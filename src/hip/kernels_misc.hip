@@ -1,0 +1,199 @@
+// State preparation, distributed pack/unpack and elementwise kernels.
+// All grid-stride, 256 threads, 16-byte vector accesses where the layout
+// allows; launched on the backend stream.
+#include "qa_hip.h"
+
+namespace qa {
+namespace hipk {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+int gridFor(long long work) {
+    long long g = (work + kThreads - 1) / kThreads;
+    long long mx = (long long)numCUs() * 16;
+    if (g > mx) g = mx;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+__device__ __forceinline__ long long ins0(long long x, int b) {
+    long long low = x & ((1ll << b) - 1);
+    return ((x >> b) << (b + 1)) | low;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void fillKernel(T* __restrict__ re, T* __restrict__ im, long long n, T vr,
+                                                       T vi) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        re[i] = vr;
+        im[i] = vi;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void debugKernel(T* __restrict__ re, T* __restrict__ im, long long n,
+                                                        long long offset) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const long long g = offset + i;
+        re[i] = (T)((g * 2.0) / 10.0);
+        im[i] = (T)((g * 2.0 + 1.0) / 10.0);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void fillBitKernel(T* __restrict__ re, T* __restrict__ im, long long n,
+                                                          int bit, int outcome, T val) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        re[i] = (((i >> bit) & 1) == outcome) ? val : (T)0;
+        im[i] = 0;
+    }
+}
+
+// gather (UNPACK=false) / scatter (UNPACK=true) of the amplitudes whose bit
+// `bit` == bitVal; VN consecutive items per thread when the runs allow it
+template <typename T, bool UNPACK, bool VEC>
+__global__ __launch_bounds__(kThreads) void packKernel(T* __restrict__ re, T* __restrict__ im, int bit, int bitVal,
+                                                       long long start, long long count, T* __restrict__ br,
+                                                       T* __restrict__ bi) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = VEC ? Vec16<T>::n : 1;
+    const long long set = (long long)bitVal << bit;
+    const long long units = count / VN;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
+        const long long j = u * VN;
+        const long long i = ins0(start + j, bit) | set;
+        if constexpr (VEC) {
+            if constexpr (UNPACK) {
+                *reinterpret_cast<V*>(re + i) = *reinterpret_cast<const V*>(br + j);
+                *reinterpret_cast<V*>(im + i) = *reinterpret_cast<const V*>(bi + j);
+            } else {
+                *reinterpret_cast<V*>(br + j) = *reinterpret_cast<const V*>(re + i);
+                *reinterpret_cast<V*>(bi + j) = *reinterpret_cast<const V*>(im + i);
+            }
+        } else {
+            if constexpr (UNPACK) {
+                re[i] = br[j];
+                im[i] = bi[j];
+            } else {
+                br[j] = re[i];
+                bi[j] = im[i];
+            }
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void axpbyKernel(T* __restrict__ ar, T* __restrict__ ai, T alpha,
+                                                        const T* __restrict__ br, const T* __restrict__ bi, T beta,
+                                                        long long n) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = Vec16<T>::n;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long nv = n / VN;
+    for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nv; u += stride) {
+        V a = reinterpret_cast<V*>(ar)[u], b = reinterpret_cast<V*>(ai)[u];
+        const V c = reinterpret_cast<const V*>(br)[u], d = reinterpret_cast<const V*>(bi)[u];
+        T* pa = reinterpret_cast<T*>(&a);
+        T* pb = reinterpret_cast<T*>(&b);
+        const T* pc = reinterpret_cast<const T*>(&c);
+        const T* pd = reinterpret_cast<const T*>(&d);
+#pragma unroll
+        for (int e = 0; e < VN; e++) {
+            pa[e] = alpha * pa[e] + beta * pc[e];
+            pb[e] = alpha * pb[e] + beta * pd[e];
+        }
+        reinterpret_cast<V*>(ar)[u] = a;
+        reinterpret_cast<V*>(ai)[u] = b;
+    }
+    for (long long i = nv * VN + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        ar[i] = alpha * ar[i] + beta * br[i];
+        ai[i] = alpha * ai[i] + beta * bi[i];
+    }
+}
+
+// rho(r, c) = psi_r conj(psi_c); consecutive threads walk consecutive rows of
+// one column, so rho writes and psi_r reads are coalesced and psi_c is a
+// broadcast (the reference gives each thread a whole row: column-strided
+// writes, QuEST_gpu.cu:67-84)
+template <typename T>
+__global__ __launch_bounds__(kThreads) void densPureKernel(T* __restrict__ re, T* __restrict__ im, long long n,
+                                                           const T* __restrict__ pr, const T* __restrict__ pi, int nq,
+                                                           long long chunkStart) {
+    const long long mask = (1ll << nq) - 1;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        const long long g = chunkStart + k, r = g & mask, c = g >> nq;
+        const T ar = pr[r], ai = pi[r], cr = pr[c], ci = pi[c];
+        re[k] = ar * cr + ai * ci;
+        im[k] = ai * cr - ar * ci;
+    }
+}
+
+}  // namespace
+
+void launchFill(real* re, real* im, i64 n, real vr, real vi) {
+    if (vr == 0 && vi == 0) {
+        QA_HIP_CHECK(hipMemsetAsync(re, 0, sizeof(real) * n, stream()));
+        QA_HIP_CHECK(hipMemsetAsync(im, 0, sizeof(real) * n, stream()));
+        return;
+    }
+    hipLaunchKernelGGL(fillKernel<real>, dim3(gridFor(n)), dim3(kThreads), 0, stream(), re, im, n, vr, vi);
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+void launchInitDebug(real* re, real* im, i64 n, i64 offset) {
+    hipLaunchKernelGGL(debugKernel<real>, dim3(gridFor(n)), dim3(kThreads), 0, stream(), re, im, n, offset);
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+void launchFillWhereBit(real* re, real* im, i64 n, int bit, int outcome, real val) {
+    hipLaunchKernelGGL(fillBitKernel<real>, dim3(gridFor(n)), dim3(kThreads), 0, stream(), re, im, n, bit, outcome,
+                       val);
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+void launchPackBit(const real* re, const real* im, int bit, int bitVal, i64 start, i64 count, real* br, real* bi,
+                   bool unpack) {
+    constexpr int VN = Vec16<real>::n;
+    const bool vec = ((1ll << bit) >= VN) && (start % VN == 0) && (count % VN == 0);
+    real* r = const_cast<real*>(re);
+    real* m = const_cast<real*>(im);
+    const int g = gridFor(vec ? count / VN : count);
+    if (unpack) {
+        if (vec)
+            hipLaunchKernelGGL((packKernel<real, true, true>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
+                               bitVal, start, count, br, bi);
+        else
+            hipLaunchKernelGGL((packKernel<real, true, false>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
+                               bitVal, start, count, br, bi);
+    } else {
+        if (vec)
+            hipLaunchKernelGGL((packKernel<real, false, true>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
+                               bitVal, start, count, br, bi);
+        else
+            hipLaunchKernelGGL((packKernel<real, false, false>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
+                               bitVal, start, count, br, bi);
+    }
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n) {
+    hipLaunchKernelGGL(axpbyKernel<real>, dim3(gridFor(n / Vec16<real>::n)), dim3(kThreads), 0, stream(), ar, ai,
+                       alpha, br, bi, beta, n);
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+void launchDensInitPure(real* re, real* im, i64 n, const real* pr, const real* pi, int nq, i64 chunkStart) {
+    hipLaunchKernelGGL(densPureKernel<real>, dim3(gridFor(n)), dim3(kThreads), 0, stream(), re, im, n, pr, pi, nq,
+                       chunkStart);
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hipk
+}  // namespace qa

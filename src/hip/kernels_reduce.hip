@@ -1,0 +1,268 @@
+// Reductions for CDNA4: probabilities, norms, inner products, density-matrix
+// traces and fidelities.
+//
+// Two launches per reduction, both deterministic (no float atomics, fixed
+// summation tree):  a grid-stride first level where each thread accumulates
+// in fp64 over 16-byte vector loads, a 64-lane wave reduction with
+// __shfl_xor, and one partial per workgroup; then a single-workgroup finish.
+// The reference instead runs one kernel per 512-element level with a
+// cudaDeviceSynchronize between levels and a divergent __syncthreads
+// (QuEST_gpu.cu:1335-1352, :1515-1551), and sums calcTotalProb on the host
+// after copying the whole state back (:1121, :1143-1163).
+#include "qa_hip.h"
+
+namespace qa {
+namespace hipk {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxBlocks = 2048;
+
+double* g_partials = nullptr;  // 2 * kMaxBlocks doubles
+double* g_out = nullptr;       // 2 doubles (device)
+double* g_outHost = nullptr;   // 2 doubles (pinned)
+
+void ensureScratch() {
+    if (g_partials) return;
+    QA_HIP_CHECK(hipMalloc(&g_partials, sizeof(double) * 2 * kMaxBlocks));
+    QA_HIP_CHECK(hipMalloc(&g_out, sizeof(double) * 2));
+    QA_HIP_CHECK(hipHostMalloc(&g_outHost, sizeof(double) * 2, hipHostMallocDefault));
+}
+
+__device__ __forceinline__ double waveSum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// sum over the block; result valid in thread 0
+__device__ __forceinline__ double blockSum(double v) {
+    __shared__ double sh[kThreads / 64];
+    v = waveSum(v);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0;
+    if (threadIdx.x < 64) {
+        r = (threadIdx.x < kThreads / 64) ? sh[threadIdx.x] : 0.0;
+        r = waveSum(r);
+    }
+    return r;
+}
+
+__device__ __forceinline__ long long ins0(long long x, int b) {
+    long long low = x & ((1ll << b) - 1);
+    return ((x >> b) << (b + 1)) | low;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void sumSqAllKernel(const T* __restrict__ re, const T* __restrict__ im,
+                                                           long long n, double* __restrict__ part) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = Vec16<T>::n;
+    double acc = 0;
+    const long long nv = n / VN;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nv; u += stride) {
+        const V a = reinterpret_cast<const V*>(re)[u];
+        const V b = reinterpret_cast<const V*>(im)[u];
+        const T* pa = reinterpret_cast<const T*>(&a);
+        const T* pb = reinterpret_cast<const T*>(&b);
+#pragma unroll
+        for (int e = 0; e < VN; e++) acc += (double)pa[e] * pa[e] + (double)pb[e] * pb[e];
+    }
+    for (long long i = nv * VN + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        acc += (double)re[i] * re[i] + (double)im[i] * im[i];
+    const double s = blockSum(acc);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// amplitudes whose bit `bit` == bitVal; VN consecutive per unit when 2^bit >= VN
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kThreads) void sumSqBitKernel(const T* __restrict__ re, const T* __restrict__ im,
+                                                           long long n, int bit, int bitVal,
+                                                           double* __restrict__ part) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = VEC ? Vec16<T>::n : 1;
+    double acc = 0;
+    const long long units = (n >> 1) / VN;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const long long set = (long long)bitVal << bit;
+    for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
+        const long long i = ins0(u * VN, bit) | set;
+        if constexpr (VEC) {
+            const V a = *reinterpret_cast<const V*>(re + i);
+            const V b = *reinterpret_cast<const V*>(im + i);
+            const T* pa = reinterpret_cast<const T*>(&a);
+            const T* pb = reinterpret_cast<const T*>(&b);
+#pragma unroll
+            for (int e = 0; e < VN; e++) acc += (double)pa[e] * pa[e] + (double)pb[e] * pb[e];
+        } else {
+            acc += (double)re[i] * re[i] + (double)im[i] * im[i];
+        }
+    }
+    const double s = blockSum(acc);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void innerKernel(const T* __restrict__ ar, const T* __restrict__ ai,
+                                                        const T* __restrict__ br, const T* __restrict__ bi,
+                                                        long long n, double* __restrict__ part) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = Vec16<T>::n;
+    double sr = 0, si = 0;
+    const long long nv = n / VN;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nv; u += stride) {
+        const V a = reinterpret_cast<const V*>(ar)[u], b = reinterpret_cast<const V*>(ai)[u];
+        const V c = reinterpret_cast<const V*>(br)[u], d = reinterpret_cast<const V*>(bi)[u];
+        const T *pa = reinterpret_cast<const T*>(&a), *pb = reinterpret_cast<const T*>(&b);
+        const T *pc = reinterpret_cast<const T*>(&c), *pd = reinterpret_cast<const T*>(&d);
+#pragma unroll
+        for (int e = 0; e < VN; e++) {
+            sr += (double)pa[e] * pc[e] + (double)pb[e] * pd[e];
+            si += (double)pa[e] * pd[e] - (double)pb[e] * pc[e];
+        }
+    }
+    for (long long i = nv * VN + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        sr += (double)ar[i] * br[i] + (double)ai[i] * bi[i];
+        si += (double)ar[i] * bi[i] - (double)ai[i] * br[i];
+    }
+    const double s0 = blockSum(sr);
+    const double s1 = blockSum(si);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = s0;
+        part[kMaxBlocks + blockIdx.x] = s1;
+    }
+}
+
+struct Offs {
+    unsigned long long o[32];
+};
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void densDiagKernel(const T* __restrict__ re, long long chunkAmps, Offs offs,
+                                                           int nq, int skipBit, long long chunkStart,
+                                                           double* __restrict__ part) {
+    double acc = 0;
+    const long long dim = skipBit >= 0 ? (1ll << (nq - 1)) : (1ll << nq);
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < dim; j += stride) {
+        const long long r = skipBit >= 0 ? ins0(j, skipBit) : j;
+        long long p = 0;
+        for (int b = 0; b < nq; b++)
+            if ((r >> b) & 1) p |= (long long)offs.o[b];
+        p -= chunkStart;
+        if (p >= 0 && p < chunkAmps) acc += (double)re[p];
+    }
+    const double s = blockSum(acc);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void densFidelityKernel(const T* __restrict__ re, const T* __restrict__ im,
+                                                               long long n, const T* __restrict__ pr,
+                                                               const T* __restrict__ pi, int nq,
+                                                               long long chunkStart, double* __restrict__ part) {
+    double acc = 0;
+    const long long mask = (1ll << nq) - 1;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        const long long g = chunkStart + k, r = g & mask, c = g >> nq;
+        const double ar = (double)re[k] * pr[c] - (double)im[k] * pi[c];
+        const double ai = (double)re[k] * pi[c] + (double)im[k] * pr[c];
+        acc += (double)pr[r] * ar + (double)pi[r] * ai;
+    }
+    const double s = blockSum(acc);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void finishKernel(const double* __restrict__ part, int nb, int nvals,
+                                                         double* __restrict__ out) {
+    for (int v = 0; v < nvals; v++) {
+        double acc = 0;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[v * kMaxBlocks + i];
+        const double s = blockSum(acc);
+        if (threadIdx.x == 0) out[v] = s;
+        __syncthreads();
+    }
+}
+
+int blocksFor(long long work) {
+    long long b = (work + kThreads * 4 - 1) / (kThreads * 4);
+    if (b < 1) b = 1;
+    if (b > kMaxBlocks) b = kMaxBlocks;
+    return (int)b;
+}
+
+void finish(int nb, int nvals, double* result) {
+    hipLaunchKernelGGL(finishKernel, dim3(1), dim3(kThreads), 0, stream(), g_partials, nb, nvals, g_out);
+    QA_HIP_CHECK(hipGetLastError());
+    QA_HIP_CHECK(hipMemcpyAsync(g_outHost, g_out, sizeof(double) * nvals, hipMemcpyDeviceToHost, stream()));
+    QA_HIP_CHECK(hipStreamSynchronize(stream()));
+    for (int v = 0; v < nvals; v++) result[v] = g_outHost[v];
+}
+
+}  // namespace
+
+double reduceSumSq(const real* re, const real* im, i64 n, int bit, int bitVal) {
+    ensureScratch();
+    constexpr int VN = Vec16<real>::n;
+    int nb;
+    if (bit < 0) {
+        nb = blocksFor(n / VN);
+        hipLaunchKernelGGL(sumSqAllKernel<real>, dim3(nb), dim3(kThreads), 0, stream(), re, im, n, g_partials);
+    } else if ((1ll << bit) >= VN) {
+        nb = blocksFor(n / 2 / VN);
+        hipLaunchKernelGGL((sumSqBitKernel<real, true>), dim3(nb), dim3(kThreads), 0, stream(), re, im, n, bit,
+                           bitVal, g_partials);
+    } else {
+        nb = blocksFor(n / 2);
+        hipLaunchKernelGGL((sumSqBitKernel<real, false>), dim3(nb), dim3(kThreads), 0, stream(), re, im, n, bit,
+                           bitVal, g_partials);
+    }
+    QA_HIP_CHECK(hipGetLastError());
+    double r;
+    finish(nb, 1, &r);
+    return r;
+}
+
+void reduceInner(const real* ar, const real* ai, const real* br, const real* bi, i64 n, double out[2]) {
+    ensureScratch();
+    const int nb = blocksFor(n / Vec16<real>::n);
+    hipLaunchKernelGGL(innerKernel<real>, dim3(nb), dim3(kThreads), 0, stream(), ar, ai, br, bi, n, g_partials);
+    QA_HIP_CHECK(hipGetLastError());
+    finish(nb, 2, out);
+}
+
+double reduceDensDiag(const real* re, i64 chunkAmps, const u64* offs, int nq, int skipBit, i64 chunkStart) {
+    ensureScratch();
+    Offs o;
+    for (int i = 0; i < 32; i++) o.o[i] = i < nq ? offs[i] : 0;
+    const long long dim = 1ll << nq;
+    const int nb = blocksFor(dim);
+    hipLaunchKernelGGL(densDiagKernel<real>, dim3(nb), dim3(kThreads), 0, stream(), re, chunkAmps, o, nq, skipBit,
+                       chunkStart, g_partials);
+    QA_HIP_CHECK(hipGetLastError());
+    double r;
+    finish(nb, 1, &r);
+    return r;
+}
+
+double reduceDensFidelity(const real* re, const real* im, i64 n, const real* pr, const real* pi, int nq,
+                          i64 chunkStart) {
+    ensureScratch();
+    const int nb = blocksFor(n);
+    hipLaunchKernelGGL(densFidelityKernel<real>, dim3(nb), dim3(kThreads), 0, stream(), re, im, n, pr, pi, nq,
+                       chunkStart, g_partials);
+    QA_HIP_CHECK(hipGetLastError());
+    double r;
+    finish(nb, 1, &r);
+    return r;
+}
+
+}  // namespace hipk
+}  // namespace qa

@@ -1,0 +1,68 @@
+// Shared declarations of the HIP (gfx950) backend translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "../core/core.hpp"
+#include "../core/tiles.hpp"
+
+#define QA_HIP_CHECK(expr)                                                                        \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) qa::hipk::fatal(#expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+    } while (0)
+
+namespace qa {
+namespace hipk {
+
+[[noreturn]] void fatal(const char* expr, const char* err, const char* file, int line);
+
+hipStream_t stream();   // the backend's compute stream (RCCL ops are ordered on it too)
+int numCUs();
+
+// vector type moving 16 bytes of amplitudes (2 doubles or 4 floats)
+template <typename T>
+struct Vec16;
+template <>
+struct Vec16<double> {
+    using type = double2;
+    static constexpr int n = 2;
+};
+template <>
+struct Vec16<float> {
+    using type = float4;
+    static constexpr int n = 4;
+};
+
+// Kernel launch parameters of one tile pass.
+struct TileArgs {
+    int L;               // local qubits of the chunk
+    int k;               // tile qubits
+    int c;               // contiguous low tile bits (pos[i] == i for i < c)
+    int nOps;
+    long long numTiles;  // 2^(L-k)
+    int pos[32];         // tile bit -> physical bit
+};
+
+// ---- launchers (defined in kernels_*.hip) ----------------------------------
+void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps);
+void launchFill(real* re, real* im, i64 n, real vr, real vi);
+void launchInitDebug(real* re, real* im, i64 n, i64 offset);
+void launchFillWhereBit(real* re, real* im, i64 n, int bit, int outcome, real val);
+void launchPackBit(const real* re, const real* im, int bit, int bitVal, i64 start, i64 count, real* br, real* bi,
+                   bool unpack);
+void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n);
+void launchDensInitPure(real* re, real* im, i64 n, const real* pr, const real* pi, int nq, i64 chunkStart);
+
+// reductions: results are written to `out` (device, doubles) and copied back
+double reduceSumSq(const real* re, const real* im, i64 n, int bit, int bitVal);
+void reduceInner(const real* ar, const real* ai, const real* br, const real* bi, i64 n, double out[2]);
+double reduceDensDiag(const real* re, i64 chunkAmps, const u64* offs, int nq, int skipBit, i64 chunkStart);
+double reduceDensFidelity(const real* re, const real* im, i64 n, const real* pr, const real* pi, int nq,
+                          i64 chunkStart);
+
+}  // namespace hipk
+}  // namespace qa

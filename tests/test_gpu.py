@@ -1,0 +1,194 @@
+"""HIP (gfx950) backend tests: every kernel family against the NumPy oracle
+(fp32/fp64 reference computations of the same ops), at qubit counts that
+exercise every tile geometry (whole-state tile, multi-tile, high targets,
+controls outside the tile) and the fused / unfused paths."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def genv():
+    import quest_amd as qa
+
+    e = qa.Env()
+    assert qa.capi.getQuESTBackend() == "HIP", "HIP library not loaded on a GPU test run"
+    return e
+
+
+def test_native_hip_library_loaded(genv):
+    from quest_amd.ops import capi
+
+    b = capi.binding()
+    assert b.backend == "hip"
+    assert b.lib._quest_path.endswith("libQuEST_hip_f64.so")
+    maps = open("/proc/self/maps").read()
+    assert "libQuEST_hip_f64.so" in maps
+
+
+@pytest.mark.parametrize("n", [3, 6, 9, 12, 15])
+def test_all_gates_vs_oracle(genv, n):
+    import quest_amd as qa
+    from helpers import GATES_1Q, GATES_2Q, apply_named, assert_close, oracle_for
+
+    rng = np.random.default_rng(n)
+    reg = qa.Register(genv, n)
+    for name in GATES_1Q:
+        for t in range(n):
+            o = oracle_for(reg, rng)
+            apply_named(reg, o, name, [t], rng)
+            assert_close(reg, o)
+    for name in GATES_2Q:
+        for _ in range(6):
+            qs = [int(x) for x in rng.permutation(n)[:2]]
+            o = oracle_for(reg, rng)
+            apply_named(reg, o, name, qs, rng)
+            assert_close(reg, o)
+    for name in ("mcunitary", "mcphase", "mcz"):
+        for k in range(2, min(n, 5) + 1):
+            qs = [int(x) for x in rng.permutation(n)[:k]]
+            o = oracle_for(reg, rng)
+            apply_named(reg, o, name, qs, rng)
+            assert_close(reg, o)
+    reg.close()
+
+
+@pytest.mark.parametrize("n", [3, 5, 7])
+def test_density_gates_and_noise(genv, n):
+    import quest_amd as qa
+    from helpers import apply_random_ops, assert_close, oracle_for
+
+    rng = np.random.default_rng(100 + n)
+    reg = qa.Register(genv, n, density=True)
+    for _ in range(3):
+        o = oracle_for(reg, rng)
+        apply_random_ops(reg, o, rng, 40, noise=True)
+        assert_close(reg, o, tol=1e-9)
+        assert abs(reg.total_prob() - np.real(np.trace(o.rho))) < 1e-10
+        assert abs(reg.purity() - o.purity()) < 1e-10
+        for q in range(n):
+            assert abs(reg.prob(q, 0) - o.prob(q, 0)) < 1e-10
+    reg.close()
+
+
+@pytest.mark.parametrize("fusion", [True, False])
+@pytest.mark.parametrize("n", [14, 20])
+def test_random_circuit_fused_and_eager(genv, n, fusion):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.utils import oracle as O
+
+    qa.capi.setGateFusion(1 if fusion else 0)
+    try:
+        c = random_layered(n, 3, seed=n)
+        reg = qa.Register(genv, n)
+        reg.init_plus()
+        c.apply(reg)
+        o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
+        c.apply_oracle(o)
+        got = reg.to_numpy()
+        assert np.max(np.abs(got - o.v)) < 1e-10
+        for q in (0, n // 2, n - 1):
+            assert abs(reg.prob(q, 1) - o.prob(q, 1)) < 1e-10
+        reg.close()
+    finally:
+        qa.capi.setGateFusion(1)
+
+
+def test_reductions_and_collapse_large(genv):
+    """24 qubits: 128 MiB per array; norm, per-qubit probabilities, inner
+    product and collapse against quantities computed from the same state."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+
+    n = 24
+    a = qa.Register(genv, n)
+    b = qa.Register(genv, n)
+    a.init_plus()
+    random_layered(n, 2, seed=3).apply(a)
+    b.clone_from(a)
+    assert abs(a.total_prob() - 1) < 1e-11
+    ip = a.inner(b)
+    assert abs(ip - 1) < 1e-11
+    v = a.to_numpy()
+    idx = np.arange(1 << n)
+    for q in (0, 1, 5, 12, 23):
+        want = float(np.sum(np.abs(v[((idx >> q) & 1) == 0]) ** 2))
+        assert abs(a.prob(q, 0) - want) < 1e-11
+    p = a.collapse(7, 1)
+    assert abs(a.total_prob() - 1) < 1e-11
+    assert a.prob(7, 1) > 1 - 1e-11
+    assert p > 0
+    a.close()
+    b.close()
+
+
+def test_measure_seeded_matches_cpu_semantics(genv):
+    """Seeded measurement reproduces the reference's expectations
+    (tests/unit/state_vector/maths/measure.test:11-45)."""
+    import quest_amd as qa
+    from quest_amd.ops import capi
+
+    q = qa.Register(genv, 3)
+    q.init_zero()
+    capi.seedQuEST([1])
+    assert [q.measure(i) for i in range(3)] == [0, 0, 0]
+    q.init_plus()
+    assert [q.measure(i) for i in range(3)] == [0, 1, 1]
+    q.close()
+
+
+def test_torch_interop(genv):
+    import torch
+
+    import quest_amd as qa
+
+    r = qa.Register(genv, 10)
+    r.init_debug()
+    t = r.to_torch()
+    i = torch.arange(1 << 10, device="cuda", dtype=torch.float64)
+    assert torch.allclose(t.real, 0.2 * i) and torch.allclose(t.imag, 0.2 * i + 0.1)
+    r.from_torch(t * 2)
+    assert abs(r.amp(3) - 2 * (0.6 + 0.7j)) < 1e-12
+    r.close()
+
+
+def test_fusion_reduces_passes(genv):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+
+    n = 22
+    c = random_layered(n, 4, seed=11)
+    reg = qa.Register(genv, n)
+    reg.init_plus()
+    qa.capi.resetQuESTStats()
+    c.apply(reg)
+    reg.sync()
+    st = qa.capi.getQuESTStats()
+    assert st["passes"] < len(c.gates) / 4, st
+    assert abs(reg.total_prob() - 1) < 1e-10
+    reg.close()
+
+
+def test_fp32_library_builds_and_loads():
+    """The fp32 HIP library is a separate compile-time build (QuEST_PREC=1);
+    check it in a subprocess (a process binds one precision)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import quest_amd as qa, math\n"
+        "e = qa.Env(); r = qa.Register(e, 12); r.init_plus(); r.h(3); r.rx(7, 0.3); r.cnot(2, 9)\n"
+        "assert abs(r.total_prob() - 1) < 1e-5\n"
+        "from quest_amd.ops import capi; assert capi.getQuEST_PREC() == 1\n"
+        "print('fp32 ok')\n"
+    )
+    envv = dict(os.environ, QUEST_PREC="1", QUEST_BACKEND="hip")
+    out = subprocess.run([sys.executable, "-c", code], env=envv, capture_output=True, text=True, timeout=300,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr
+    assert "fp32 ok" in out.stdout
