@@ -28,6 +28,12 @@ int getGateFusion(void);
 /* Maximum number of qubits spanned by one fused pass (0 = default). */
 void setFusionMaxQubits(int numQubits);
 
+/* Backend tuning knobs (HIP build): "direct_kernels" (LDS-free kernel for a
+ * pass holding one gate), "tile_mode" (0 op by op, 1 register phases, 2 dense blocks),
+ * "tile_wg_per_cu".  Returns 1 if the key is known.  Also settable at start
+ * via QUEST_DIRECT_KERNELS / QUEST_TILE_MODE / QUEST_TILE_WG_PER_CU. */
+int setQuESTTuning(const char* key, int value);
+
 /* Submit every queued operation of the register to the device (async). */
 void flushQureg(Qureg qureg);
 /* flushQureg + wait for the device. */

@@ -138,6 +138,7 @@ class _Binding:
             "setDensityAmps": (v, [Q, rp, rp]), "getQuEST_PREC": (i, []),
             # MI355X extensions
             "setGateFusion": (v, [i]), "getGateFusion": (i, []), "setFusionMaxQubits": (v, [i]),
+            "setQuESTTuning": (i, [C.c_char_p, i]),
             "flushQureg": (v, [Q]), "syncQureg": (v, [Q]), "copyStateToGPU": (v, [Q]),
             "copyStateFromGPU": (v, [Q]), "copyChunkToBuffers": (v, [Q, C.c_void_p, C.c_void_p]),
             "copyChunkFromBuffers": (v, [Q, C.c_void_p, C.c_void_p]), "canonicaliseQureg": (v, [Q]),
@@ -402,6 +403,10 @@ def getQuESTStats() -> dict:
     s = b.QuESTStats()
     _call("getQuESTStats", C.byref(s))
     return {n: getattr(s, n) for n, _ in b.QuESTStats._fields_}
+
+
+def setQuESTTuning(key: str, value: int) -> bool:
+    return bool(_call("setQuESTTuning", key.encode(), int(value)))
 
 
 def getQuESTBackend() -> str:

@@ -886,6 +886,11 @@ void setFusionMaxQubits(int numQubits) {
     rt().fuseMaxQubits = numQubits;
 }
 
+int setQuESTTuning(const char* key, int value) {
+    for (QuregImpl* q : liveQuregs()) be::flush(*q);
+    return be::setTuning(key, value) ? 1 : 0;
+}
+
 void flushQureg(Qureg qureg) { router::flush(Q(qureg)); }
 void syncQureg(Qureg qureg) { router::sync(Q(qureg)); }
 

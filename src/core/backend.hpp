@@ -20,6 +20,7 @@ void deviceSync();                 // wait for all queued device work
 std::string describe();            // device/backend description for reports
 const char* shortName();           // "HIP" or "CPU"
 bool stateOnHost();                // CPU build: amplitudes are host memory
+bool setTuning(const char* key, int value);  // backend knobs; false if unknown
 
 // ---- memory --------------------------------------------------------------
 void allocState(QuregImpl& q);     // sets q.re / q.im (numAmpsPerChunk each)

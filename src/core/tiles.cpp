@@ -86,4 +86,293 @@ void planTiles(const std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse,
     emitPass(ops, begin, (int)ops.size(), cur, L, k, c, out);
 }
 
+namespace {
+
+struct PhaseBuilder {
+    int R;
+    int k;
+    std::vector<int> regs;   // ordered register tile bits (fixed prefix first)
+    int fixed = 0;           // leading regs whose order is pinned (Mat4 pair / quad)
+    int begin = 0;
+    bool open = false;
+
+    bool has(int b) const {
+        for (int r : regs)
+            if (r == b) return true;
+        return false;
+    }
+};
+
+// LDS slot (8-byte word mod 32) contribution of tile bit b under ldsSwizzle.
+unsigned slotVector(int b) { return ldsSwizzle(1u << b) & 31u; }
+
+int gf2Rank(const std::vector<unsigned>& vs) {
+    std::vector<unsigned> basis;
+    for (unsigned v : vs) {
+        for (unsigned x : basis) v = std::min(v, v ^ x);
+        if (v) basis.push_back(v);
+    }
+    return (int)basis.size();
+}
+
+// Lanes 0-31 of a half-wave vary the first 5 lane bits: pick non-register
+// tile bits whose slot vectors are independent (conflict-free), lowest first,
+// then the rest in ascending order.
+void assignLanes(TilePhase& ph, int k, int R) {
+    std::vector<int> nonreg;
+    for (int b = 0; b < k; b++) {
+        bool isReg = false;
+        for (int r = 0; r < R; r++) isReg |= (ph.reg[r] == b);
+        if (!isReg) nonreg.push_back(b);
+    }
+    std::vector<int> order;
+    std::vector<unsigned> vecs;
+    std::vector<bool> used(nonreg.size(), false);
+    for (size_t i = 0; i < nonreg.size() && order.size() < 5; i++) {
+        std::vector<unsigned> trial = vecs;
+        trial.push_back(slotVector(nonreg[i]));
+        if (gf2Rank(trial) == (int)trial.size()) {
+            vecs = trial;
+            order.push_back(nonreg[i]);
+            used[i] = true;
+        }
+    }
+    for (size_t i = 0; i < nonreg.size(); i++)
+        if (!used[i]) order.push_back(nonreg[i]);
+    for (size_t i = 0; i < order.size() && i < 16; i++) ph.lane[i] = order[i];
+}
+
+void closePhase(PhaseBuilder& pb, int end, TileProgram& prog) {
+    if (!pb.open || end <= pb.begin) {
+        pb.open = false;
+        pb.regs.clear();
+        pb.fixed = 0;
+        return;
+    }
+    TilePhase ph;
+    ph.opBegin = pb.begin;
+    ph.opEnd = end;
+    ph.lds = 0;
+    // pad with unused tile bits, lowest first
+    std::vector<int> regs = pb.regs;
+    for (int b = 0; (int)regs.size() < pb.R && b < pb.k; b++) {
+        bool used = false;
+        for (int r : regs) used |= (r == b);
+        if (!used) regs.push_back(b);
+    }
+    for (int r = 0; r < pb.R; r++) ph.reg[r] = regs[r];
+    assignLanes(ph, pb.k, pb.R);
+    for (int o = pb.begin; o < end; o++) {
+        TileOp& op = prog.ops[o];
+        int nt = op.kind == (int)OpKind::Mat2 ? 1 : op.kind == (int)OpKind::Mat4 ? 2
+                 : op.kind == (int)OpKind::DensChan2 ? 4 : 0;
+        for (int j = 0; j < nt; j++)
+            for (int r = 0; r < pb.R; r++)
+                if (ph.reg[r] == op.t[j]) op.rt[j] = r;
+    }
+    prog.phases.push_back(ph);
+    pb.open = false;
+    pb.regs.clear();
+    pb.fixed = 0;
+}
+
+void startPhase(PhaseBuilder& pb, int at) {
+    pb.open = true;
+    pb.begin = at;
+    pb.regs.clear();
+    pb.fixed = 0;
+}
+
+}  // namespace
+
+namespace {
+
+// qubits (tile bits) an op touches: targets + in-tile controls / phase bits
+unsigned opQubits(const TileOp& op) {
+    unsigned m = op.ctrlIn;
+    const int nt = op.kind == (int)OpKind::Mat2 ? 1 : op.kind == (int)OpKind::Mat4 ? 2
+                   : op.kind == (int)OpKind::DensChan2 ? 4 : 0;
+    for (int j = 0; j < nt; j++) m |= 1u << op.t[j];
+    return m;
+}
+
+// apply one op to a 2^R block vector; loc[b] = block slot of tile bit b
+void applyToBlock(const TileOp& op, const int* loc, int R, std::vector<cplx>& v) {
+    const int M = 1 << R;
+    unsigned cmask = 0;
+    for (int b = 0; b < 32; b++)
+        if ((op.ctrlIn >> b) & 1u) cmask |= 1u << loc[b];
+    auto cm = [&](int r, int c) -> cplx { return {op.m[2 * (r * (op.kind == (int)OpKind::Mat2 ? 2 : 4) + c)],
+                                                  op.m[2 * (r * (op.kind == (int)OpKind::Mat2 ? 2 : 4) + c) + 1]}; };
+    if (op.kind == (int)OpKind::Diag) {
+        const cplx t = {op.m[0], op.m[1]};
+        for (int j = 0; j < M; j++)
+            if (((unsigned)j & cmask) == cmask) v[j] = cmul(t, v[j]);
+        return;
+    }
+    if (op.kind == (int)OpKind::Mat2) {
+        const int a = loc[op.t[0]];
+        for (int j = 0; j < M; j++) {
+            if ((j >> a) & 1) continue;
+            if (((unsigned)j & cmask) != cmask) continue;
+            const int f = j | (1 << a);
+            const cplx x = v[j], y = v[f];
+            v[j] = cadd(cmul(cm(0, 0), x), cmul(cm(0, 1), y));
+            v[f] = cadd(cmul(cm(1, 0), x), cmul(cm(1, 1), y));
+        }
+        return;
+    }
+    // Mat4
+    const int a = loc[op.t[0]], b = loc[op.t[1]];
+    for (int j = 0; j < M; j++) {
+        if (((j >> a) & 1) || ((j >> b) & 1)) continue;
+        if (((unsigned)j & cmask) != cmask) continue;
+        int idx[4];
+        cplx x[4];
+        for (int g = 0; g < 4; g++) {
+            idx[g] = j | ((g & 1) << a) | ((g >> 1) << b);
+            x[g] = v[idx[g]];
+        }
+        for (int r = 0; r < 4; r++) {
+            cplx s = {0, 0};
+            for (int c = 0; c < 4; c++) s = cadd(s, cmul(cm(r, c), x[c]));
+            v[idx[r]] = s;
+        }
+    }
+}
+
+void emitDenseBlock(TileProgram& prog, int k, int R, unsigned bmask, int b, int e) {
+    TilePhase ph;
+    ph.opBegin = b;
+    ph.opEnd = e;
+    ph.lds = 0;
+    int n = 0;
+    for (int bit = 0; bit < k && n < R; bit++)
+        if ((bmask >> bit) & 1u) ph.reg[n++] = bit;
+    for (int bit = 0; bit < k && n < R; bit++)
+        if (!((bmask >> bit) & 1u)) ph.reg[n++] = bit;
+    int loc[32];
+    for (int i = 0; i < 32; i++) loc[i] = 0;
+    for (int r = 0; r < R; r++) loc[ph.reg[r]] = r;
+    const int M = 1 << R;
+    ph.mat = (int)(prog.mats.size() / (2 * M * M));
+    const size_t base = prog.mats.size();
+    prog.mats.resize(base + 2 * M * M);
+    std::vector<cplx> v(M);
+    for (int c = 0; c < M; c++) {
+        for (int j = 0; j < M; j++) v[j] = {j == c ? (real)1 : (real)0, 0};
+        for (int o = b; o < e; o++) applyToBlock(prog.ops[o], loc, R, v);
+        for (int r = 0; r < M; r++) {
+            prog.mats[base + 2 * (r * M + c)] = v[r].re;
+            prog.mats[base + 2 * (r * M + c) + 1] = v[r].im;
+        }
+    }
+    assignLanes(ph, k, R);
+    prog.phases.push_back(ph);
+}
+
+}  // namespace
+
+void planDenseBlocks(TileProgram& prog, int k, int R) {
+    prog.phases.clear();
+    prog.mats.clear();
+    for (TilePass& ps : prog.passes) {
+        ps.phaseBegin = ps.phaseEnd = (int)prog.phases.size();
+        if (k >= 0 ? ps.k != k : ps.k <= R) continue;
+        unsigned cur = 0;
+        int begin = ps.opBegin;
+        for (int o = ps.opBegin; o < ps.opEnd; o++) {
+            const TileOp& op = prog.ops[o];
+            const unsigned s = opQubits(op);
+            const bool fusable = op.ctrlOut == 0 && op.kind != (int)OpKind::DensChan2 && __builtin_popcount(s) <= R;
+            if (fusable && __builtin_popcount(cur | s) <= R) {
+                cur |= s;
+                continue;
+            }
+            if (o > begin) emitDenseBlock(prog, ps.k, R, cur, begin, o);
+            if (!fusable) {
+                TilePhase ph;
+                ph.opBegin = o;
+                ph.opEnd = o + 1;
+                ph.lds = 1;
+                prog.phases.push_back(ph);
+                begin = o + 1;
+                cur = 0;
+            } else {
+                begin = o;
+                cur = s;
+            }
+        }
+        if (ps.opEnd > begin) emitDenseBlock(prog, ps.k, R, cur, begin, ps.opEnd);
+        ps.phaseEnd = (int)prog.phases.size();
+    }
+}
+
+void planPhases(TileProgram& prog, int k, int R) {
+    prog.phases.clear();
+    for (TilePass& ps : prog.passes) {
+        ps.phaseBegin = ps.phaseEnd = (int)prog.phases.size();
+        if (k >= 0 ? ps.k != k : ps.k <= R) continue;
+        PhaseBuilder pb;
+        pb.R = R;
+        pb.k = ps.k;
+        for (int o = ps.opBegin; o < ps.opEnd; o++) {
+            TileOp& op = prog.ops[o];
+            const OpKind kind = (OpKind)op.kind;
+            if (!pb.open) startPhase(pb, o);
+            if (kind == OpKind::Diag) continue;  // no register constraint
+            if (kind == OpKind::Mat2) {
+                const int t = op.t[0];
+                if (pb.has(t)) continue;
+                if ((int)pb.regs.size() < R) {
+                    pb.regs.push_back(t);
+                    continue;
+                }
+                closePhase(pb, o, prog);
+                startPhase(pb, o);
+                pb.regs.push_back(t);
+                continue;
+            }
+            if (kind == OpKind::Mat4 && R >= 2) {
+                const int a = op.t[0], b = op.t[1];
+                bool samePair = pb.fixed == 2 && pb.regs[0] == a && pb.regs[1] == b;
+                if (samePair) continue;
+                if (pb.fixed == 0) {
+                    // pin (a, b) in slots 0, 1 if everything fits
+                    std::vector<int> nr = {a, b};
+                    for (int r : pb.regs)
+                        if (r != a && r != b) nr.push_back(r);
+                    if ((int)nr.size() <= R) {
+                        pb.regs = nr;
+                        pb.fixed = 2;
+                        continue;
+                    }
+                }
+                closePhase(pb, o, prog);
+                startPhase(pb, o);
+                pb.regs = {a, b};
+                pb.fixed = 2;
+                continue;
+            }
+            if (kind == OpKind::DensChan2 && R >= 4) {
+                closePhase(pb, o, prog);
+                startPhase(pb, o);
+                pb.regs = {op.t[0], op.t[1], op.t[2], op.t[3]};
+                pb.fixed = 4;
+                closePhase(pb, o + 1, prog);
+                continue;
+            }
+            // fallback: op applied directly on the LDS tile
+            closePhase(pb, o, prog);
+            TilePhase ph;
+            ph.opBegin = o;
+            ph.opEnd = o + 1;
+            ph.lds = 1;
+            prog.phases.push_back(ph);
+        }
+        closePhase(pb, ps.opEnd, prog);
+        ps.phaseEnd = (int)prog.phases.size();
+    }
+}
+
 }  // namespace qa

@@ -25,11 +25,41 @@ namespace qa {
 struct TileOp {
     int kind;            // OpKind
     int t[4];            // tile-local target bits
+    int rt[4];           // register slots of the targets inside a register phase
     unsigned ctrlIn;     // tile-local mask of bits that must be 1
     unsigned pad;
     u64 ctrlOut;         // physical bits outside the tile that must be 1
     real m[32];          // matrix, interleaved re/im, row-major
 };
+
+// A phase of a pass: a run of ops executed with each thread holding 2^R
+// amplitudes in registers, namely the tile elements spanned by the R tile
+// bits reg[0..R-1] (reg slot r <-> tile bit reg[r]).  Ops whose targets are
+// register bits run without touching LDS; only phase boundaries re-shuffle
+// the tile through LDS.  `lds` = 1 marks a fallback phase whose ops are
+// applied directly on the LDS tile (ops that do not fit the register scheme).
+struct TilePhase {
+    int opBegin = 0, opEnd = 0;
+    int lds = 0;
+    int mat = -1;        // >= 0: dense block phase, matrix index in TileProgram::mats
+    int reg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // tile bit carried by bit i of the thread index (the non-register bits,
+    // ordered so that the 32 lanes of a half-wave hit 32 distinct LDS slots
+    // under the GPU's XOR swizzle, see ldsSwizzle below)
+    int lane[16] = {0};
+};
+
+// XOR swizzle of the GPU tile layout in LDS: element p of a tile lives at
+// p ^ h(p >> 5).  With it, for (almost) any choice of register bits there is
+// an assignment of lanes to the remaining bits that makes every 8-byte LDS
+// access of a half-wave conflict-free (32 distinct 8-byte slots mod 256 B).
+inline unsigned ldsSwizzleHash(unsigned hi) {
+    unsigned h = hi & 31u;
+    if ((hi >> 5) & 1u) h ^= 31u;
+    if ((hi >> 6) & 1u) h ^= 21u;
+    return h;
+}
+inline unsigned ldsSwizzle(unsigned p) { return p ^ ldsSwizzleHash(p >> 5); }
 
 struct TilePass {
     int k = 0;           // tile qubits
@@ -37,12 +67,29 @@ struct TilePass {
     u64 qmask = 0;       // physical mask of Q
     int opBegin = 0;     // range in the program's op array
     int opEnd = 0;
+    int phaseBegin = 0;  // range in the program's phase array (0,0: no phases)
+    int phaseEnd = 0;
 };
 
 struct TileProgram {
     std::vector<TilePass> passes;
     std::vector<TileOp> ops;
+    std::vector<TilePhase> phases;
+    // dense block matrices: 2^R x 2^R complex, row-major, interleaved re/im
+    std::vector<real> mats;
 };
+
+// Fuse the ops of every pass with exactly `k` tile bits into dense blocks of
+// at most R qubits (the product of the block's gates, computed on the host):
+// each block is one register phase with one 2^R x 2^R matrix-vector product
+// per thread, i.e. ONE LDS round trip however many gates it absorbed.  Ops
+// with controls outside the tile, or more than R qubits, become LDS phases.
+void planDenseBlocks(TileProgram& prog, int k, int R);
+
+// Split every pass with exactly `k` tile bits (k < 0: every pass with more
+// than R tile bits) into register phases of R slots (fills TileOp::rt and
+// TileProgram::phases).
+void planPhases(TileProgram& prog, int k, int R);
 
 // Split `ops` (physical local positions, L local qubits) into passes of at
 // most kmax tile qubits (kmax >= cmin + 4).  With fuse=false every op gets its

@@ -112,6 +112,162 @@ void applyTileOp(const TileOp& op, int k, real* re, real* im) {
     }
 }
 
+// Register-phase emulation: exactly the per-thread decomposition of the GPU
+// kernel (src/hip/kernels_gates.hip), so the planner's register assignment is
+// validated on CPU.  "Thread" tau owns the 2^R tile elements tb | regOff[j].
+constexpr int kMaxRegSlots = 4;
+int regSlots() {
+    static int r = [] {
+        const char* e = getenv("QUEST_CPU_REG_SLOTS");
+        int v = e ? atoi(e) : 3;
+        return v < 2 ? 2 : v > kMaxRegSlots ? kMaxRegSlots : v;
+    }();
+    return r;
+}
+
+void applyRegOp(const TileOp& op, int R, real* vr, real* vi, unsigned tb, const unsigned* regOff) {
+    const int M = 1 << R;
+    switch ((OpKind)op.kind) {
+        case OpKind::Mat2: {
+            const int a = op.rt[0];
+            const real* m = op.m;
+            for (int j = 0; j < M; j++) {
+                if ((j >> a) & 1) continue;
+                if (((tb | regOff[j]) & op.ctrlIn) != op.ctrlIn) continue;
+                const int f = j | (1 << a);
+                real r0 = vr[j], i0 = vi[j], r1 = vr[f], i1 = vi[f];
+                vr[j] = m[0] * r0 - m[1] * i0 + m[2] * r1 - m[3] * i1;
+                vi[j] = m[0] * i0 + m[1] * r0 + m[2] * i1 + m[3] * r1;
+                vr[f] = m[4] * r0 - m[5] * i0 + m[6] * r1 - m[7] * i1;
+                vi[f] = m[4] * i0 + m[5] * r0 + m[6] * i1 + m[7] * r1;
+            }
+            break;
+        }
+        case OpKind::Diag:
+            for (int j = 0; j < M; j++) {
+                if (((tb | regOff[j]) & op.ctrlIn) != op.ctrlIn) continue;
+                real r = vr[j], i = vi[j];
+                vr[j] = op.m[0] * r - op.m[1] * i;
+                vi[j] = op.m[0] * i + op.m[1] * r;
+            }
+            break;
+        case OpKind::Mat4: {
+            const int a = op.rt[0], b = op.rt[1];
+            for (int j = 0; j < M; j++) {
+                if (((j >> a) & 1) || ((j >> b) & 1)) continue;
+                if (((tb | regOff[j]) & op.ctrlIn) != op.ctrlIn) continue;
+                int idx[4];
+                real xr[4], xi[4];
+                for (int g = 0; g < 4; g++) {
+                    idx[g] = j | ((g & 1) << a) | ((g >> 1) << b);
+                    xr[g] = vr[idx[g]];
+                    xi[g] = vi[idx[g]];
+                }
+                for (int r = 0; r < 4; r++) {
+                    real sr = 0, si = 0;
+                    for (int c = 0; c < 4; c++) {
+                        const real mr = op.m[2 * (4 * r + c)], mi = op.m[2 * (4 * r + c) + 1];
+                        sr += mr * xr[c] - mi * xi[c];
+                        si += mr * xi[c] + mi * xr[c];
+                    }
+                    vr[idx[r]] = sr;
+                    vi[idx[r]] = si;
+                }
+            }
+            break;
+        }
+        case OpKind::DensChan2: {
+            const int* s = op.rt;
+            for (int j = 0; j < M; j++) {
+                bool base = true;
+                for (int x = 0; x < 4; x++) base &= !((j >> s[x]) & 1);
+                if (!base) continue;
+                int idx[16];
+                for (int e = 0; e < 16; e++) {
+                    idx[e] = j;
+                    for (int x = 0; x < 4; x++)
+                        if ((e >> x) & 1) idx[e] |= 1 << s[x];
+                }
+                real sr = 0, si = 0;
+                for (int a = 0; a < 4; a++) {
+                    sr += vr[idx[a + 4 * a]];
+                    si += vi[idx[a + 4 * a]];
+                }
+                for (int e = 0; e < 16; e++) {
+                    if ((e & 3) != (e >> 2)) {
+                        vr[idx[e]] *= op.m[0];
+                        vi[idx[e]] *= op.m[0];
+                    } else {
+                        vr[idx[e]] = op.m[2] * vr[idx[e]] + op.m[4] * sr / 4;
+                        vi[idx[e]] = op.m[2] * vi[idx[e]] + op.m[4] * si / 4;
+                    }
+                }
+            }
+            break;
+        }
+    }
+}
+
+void runPhase(const TilePhase& ph, const TileProgram& prog, int k, i64 base, real* br, real* bi) {
+    if (ph.lds) {
+        for (int o = ph.opBegin; o < ph.opEnd; o++) {
+            const TileOp& op = prog.ops[o];
+            if (((u64)base & op.ctrlOut) == op.ctrlOut) applyTileOp(op, k, br, bi);
+        }
+        return;
+    }
+    const int R = regSlots(), M = 1 << R;
+    unsigned regMask = 0, regOff[1 << kMaxRegSlots];
+    for (int r = 0; r < R; r++) regMask |= 1u << ph.reg[r];
+    for (int j = 0; j < M; j++) {
+        regOff[j] = 0;
+        for (int r = 0; r < R; r++)
+            if ((j >> r) & 1) regOff[j] |= 1u << ph.reg[r];
+    }
+    real vr[1 << kMaxRegSlots], vi[1 << kMaxRegSlots];
+    for (unsigned tau = 0; tau < (1u << (k - R)); tau++) {
+        unsigned tb = 0, x = tau;
+        for (int b = 0; b < k; b++) {
+            if ((regMask >> b) & 1) continue;
+            tb |= (x & 1u) << b;
+            x >>= 1;
+        }
+        for (int j = 0; j < M; j++) {
+            vr[j] = br[tb | regOff[j]];
+            vi[j] = bi[tb | regOff[j]];
+        }
+        if (ph.mat >= 0) {
+            // dense block: y = U x with the host-composed 2^R x 2^R matrix
+            const real* U = prog.mats.data() + (size_t)ph.mat * 2 * M * M;
+            real yr[1 << kMaxRegSlots], yi[1 << kMaxRegSlots];
+            for (int r = 0; r < M; r++) {
+                real sr = 0, si = 0;
+                for (int c = 0; c < M; c++) {
+                    const real ur = U[2 * (r * M + c)], ui = U[2 * (r * M + c) + 1];
+                    sr += ur * vr[c] - ui * vi[c];
+                    si += ur * vi[c] + ui * vr[c];
+                }
+                yr[r] = sr;
+                yi[r] = si;
+            }
+            for (int j = 0; j < M; j++) {
+                vr[j] = yr[j];
+                vi[j] = yi[j];
+            }
+        } else {
+            for (int o = ph.opBegin; o < ph.opEnd; o++) {
+                const TileOp& op = prog.ops[o];
+                if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
+                applyRegOp(op, R, vr, vi, tb, regOff);
+            }
+        }
+        for (int j = 0; j < M; j++) {
+            br[tb | regOff[j]] = vr[j];
+            bi[tb | regOff[j]] = vi[j];
+        }
+    }
+}
+
 void runProgram(QuregImpl& q, const TileProgram& prog) {
     for (const TilePass& ps : prog.passes) {
         const unsigned n = 1u << ps.k;
@@ -125,10 +281,15 @@ void runProgram(QuregImpl& q, const TileProgram& prog) {
                 br[p] = q.re[base + offs[p]];
                 bi[p] = q.im[base + offs[p]];
             }
-            for (int o = ps.opBegin; o < ps.opEnd; o++) {
-                const TileOp& op = prog.ops[o];
-                if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
-                applyTileOp(op, ps.k, br.data(), bi.data());
+            if (ps.phaseEnd > ps.phaseBegin) {
+                for (int h = ps.phaseBegin; h < ps.phaseEnd; h++)
+                    runPhase(prog.phases[h], prog, ps.k, base, br.data(), bi.data());
+            } else {
+                for (int o = ps.opBegin; o < ps.opEnd; o++) {
+                    const TileOp& op = prog.ops[o];
+                    if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
+                    applyTileOp(op, ps.k, br.data(), bi.data());
+                }
             }
             for (unsigned p = 0; p < n; p++) {
                 q.re[base + offs[p]] = br[p];
@@ -183,6 +344,15 @@ void flush(QuregImpl& q) {
     if (q.pending.empty()) return;
     TileProgram prog;
     planTiles(q.pending, q.L, fuseQubits(), 4, rt().fusion, prog);
+    // QUEST_CPU_PLANNER: 0 op by op, 1 register phases, 2 dense blocks (default)
+    static const int planner = [] {
+        const char* e = getenv("QUEST_CPU_PLANNER");
+        return e ? atoi(e) : 2;
+    }();
+    if (planner == 1)
+        planPhases(prog, -1, regSlots());
+    else if (planner == 2)
+        planDenseBlocks(prog, -1, regSlots());
     q.pending.clear();
     runProgram(q, prog);
 }
@@ -341,5 +511,11 @@ void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* br, const real* bi) 
 void bufferToHost(const real* buf, real* host, i64 n) { memcpy(host, buf, sizeof(real) * n); }
 void hostToBuffer(const real* host, real* buf, i64 n) { memcpy(buf, host, sizeof(real) * n); }
 
+}  // namespace be
+}  // namespace qa
+
+namespace qa {
+namespace be {
+bool setTuning(const char*, int) { return false; }
 }  // namespace be
 }  // namespace qa

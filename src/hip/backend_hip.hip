@@ -35,6 +35,21 @@ bool g_slotUsed[kSlots];
 int g_nextSlot = 0;
 }  // namespace
 
+Tuning& tuning() {
+    static Tuning t = [] {
+        Tuning x;
+        auto env = [](const char* n, int d) {
+            const char* e = getenv(n);
+            return e ? atoi(e) : d;
+        };
+        x.directKernels = env("QUEST_DIRECT_KERNELS", 1);
+        x.tileMode = env("QUEST_TILE_MODE", 2);
+        x.tileWgPerCU = env("QUEST_TILE_WG_PER_CU", 2);
+        return x;
+    }();
+    return t;
+}
+
 void fatal(const char* expr, const char* err, const char* file, int line) {
     fprintf(stderr, "QuEST HIP error: %s failed: %s (%s:%d)\n", expr, err, file, line);
     fflush(stderr);
@@ -69,28 +84,48 @@ int contiguousLow(const TilePass& ps) {
     return c;
 }
 
-void runProgram(QuregImpl& q, const TileProgram& prog) {
-    const size_t bytes = sizeof(TileOp) * prog.ops.size();
-    if (bytes > kSlotBytes) fatal("tile program", "too many ops in one flush", __FILE__, __LINE__);
+bool directEnabled() { return tuning().directKernels != 0; }
+
+void runProgram(QuregImpl& q, const std::vector<Op>& src, TileProgram& prog) {
+    // phase op ranges relative to their pass (the kernel sees the pass's ops)
+    std::vector<TilePhase> rel = prog.phases;
+    for (const TilePass& ps : prog.passes)
+        for (int h = ps.phaseBegin; h < ps.phaseEnd; h++) {
+            rel[h].opBegin -= ps.opBegin;
+            rel[h].opEnd -= ps.opBegin;
+        }
+    const size_t opBytes = sizeof(TileOp) * prog.ops.size();
+    const size_t phBytes = sizeof(TilePhase) * rel.size();
+    const size_t matBytes = sizeof(real) * prog.mats.size();
+    const size_t total = opBytes + phBytes + matBytes;
+    if (total > kSlotBytes) fatal("tile program", "too many ops in one flush", __FILE__, __LINE__);
     const int s = g_nextSlot;
     g_nextSlot = (g_nextSlot + 1) % kSlots;
     if (g_slotUsed[s]) QA_HIP_CHECK(hipEventSynchronize(g_slotEvent[s]));
     char* h = g_progHost + s * kSlotBytes;
     char* d = g_progDev + s * kSlotBytes;
-    memcpy(h, prog.ops.data(), bytes);
-    QA_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, g_stream));
+    memcpy(h, prog.ops.data(), opBytes);
+    if (phBytes) memcpy(h + opBytes, rel.data(), phBytes);
+    if (matBytes) memcpy(h + opBytes + phBytes, prog.mats.data(), matBytes);
+    QA_HIP_CHECK(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, g_stream));
     const TileOp* dOps = reinterpret_cast<const TileOp*>(d);
+    const TilePhase* dPh = reinterpret_cast<const TilePhase*>(d + opBytes);
+    const real* dMats = reinterpret_cast<const real*>(d + opBytes + phBytes);
     for (const TilePass& ps : prog.passes) {
+        const int nOps = ps.opEnd - ps.opBegin;
+        stats().passes++;
+        if (nOps > 1) stats().fusedOps += nOps;
+        if (nOps == 1 && directEnabled() && launchDirectOp(q.re, q.im, q.L, src[ps.opBegin])) continue;
         TileArgs a;
         a.L = q.L;
         a.k = ps.k;
         a.c = contiguousLow(ps);
-        a.nOps = ps.opEnd - ps.opBegin;
+        a.nOps = nOps;
+        a.nPhases = ps.phaseEnd - ps.phaseBegin;
+        a.pad = 0;
         a.numTiles = 1ll << (q.L - ps.k);
         for (int i = 0; i < 32; i++) a.pos[i] = i < ps.k ? ps.pos[i] : 0;
-        launchTilePass(q.re, q.im, a, dOps + ps.opBegin);
-        stats().passes++;
-        if (a.nOps > 1) stats().fusedOps += a.nOps;
+        launchTilePass(q.re, q.im, a, dOps + ps.opBegin, dPh + ps.phaseBegin, dMats, tuning().tileMode);
     }
     QA_HIP_CHECK(hipEventRecord(g_slotEvent[s], g_stream));
     g_slotUsed[s] = true;
@@ -180,8 +215,13 @@ void flush(QuregImpl& q) {
     if (q.pending.empty()) return;
     TileProgram prog;
     planTiles(q.pending, q.L, tileQubits(q.L), sizeof(real) == 8 ? 4 : 5, rt().fusion, prog);
-    q.pending.clear();
-    runProgram(q, prog);
+    if (tuning().tileMode == 1)
+        planPhases(prog, kTileQubits, kRegSlots);
+    else if (tuning().tileMode == 2)
+        planDenseBlocks(prog, kTileQubits, kRegSlots);
+    std::vector<Op> src;
+    src.swap(q.pending);
+    runProgram(q, src, prog);
 }
 
 void fill(QuregImpl& q, real re, real im) {
@@ -290,5 +330,18 @@ void hostToBuffer(const real* host, real* buf, i64 n) {
     QA_HIP_CHECK(hipStreamSynchronize(g_stream));
 }
 
+}  // namespace be
+}  // namespace qa
+
+namespace qa {
+namespace be {
+bool setTuning(const char* key, int value) {
+    std::string k(key);
+    if (k == "direct_kernels") hipk::tuning().directKernels = value;
+    else if (k == "tile_mode") hipk::tuning().tileMode = value;
+    else if (k == "tile_wg_per_cu") hipk::tuning().tileWgPerCU = value;
+    else return false;
+    return true;
+}
 }  // namespace be
 }  // namespace qa

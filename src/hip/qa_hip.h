@@ -23,6 +23,14 @@ namespace hipk {
 hipStream_t stream();   // the backend's compute stream (RCCL ops are ordered on it too)
 int numCUs();
 
+// runtime knobs (env QUEST_* at start-up, setQuESTTuning() afterwards)
+struct Tuning {
+    int directKernels = 1;  // LDS-free kernels for single-op passes
+    int tileMode = 2;       // fused tiles: 0 op by op, 1 register phases, 2 dense blocks
+    int tileWgPerCU = 2;    // grid of the register-phase tile kernel, per CU
+};
+Tuning& tuning();
+
 // vector type moving 16 bytes of amplitudes (2 doubles or 4 floats)
 template <typename T>
 struct Vec16;
@@ -37,18 +45,28 @@ struct Vec16<float> {
     static constexpr int n = 4;
 };
 
+// Tile size of the compile-time tile kernel (2^K amplitudes, 256 threads x
+// 2^(K-8) registers): 32 KiB of LDS for fp64 and fp32 alike.
+constexpr int kTileQubits = sizeof(real) == 8 ? 11 : 12;
+constexpr int kRegSlots = kTileQubits - 8;
+
 // Kernel launch parameters of one tile pass.
 struct TileArgs {
     int L;               // local qubits of the chunk
     int k;               // tile qubits
     int c;               // contiguous low tile bits (pos[i] == i for i < c)
     int nOps;
+    int nPhases;         // register phases (0: op-by-op on LDS)
+    int pad;
     long long numTiles;  // 2^(L-k)
     int pos[32];         // tile bit -> physical bit
 };
 
 // ---- launchers (defined in kernels_*.hip) ----------------------------------
-void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps);
+void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps, const TilePhase* dPhases,
+                    const real* dMats, int mode);
+// one-op pass as a streaming kernel without LDS; false if not applicable
+bool launchDirectOp(real* re, real* im, int L, const Op& op);
 void launchFill(real* re, real* im, i64 n, real vr, real vi);
 void launchInitDebug(real* re, real* im, i64 n, i64 offset);
 void launchFillWhereBit(real* re, real* im, i64 n, int bit, int outcome, real val);
