@@ -59,7 +59,7 @@ void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k,
 
 }  // namespace
 
-void planTiles(const std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out) {
+void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out) {
     out.passes.clear();
     out.ops.clear();
     if (ops.empty()) return;
@@ -68,22 +68,47 @@ void planTiles(const std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse,
     const u64 low = (c >= 64) ? ~0ull : ((1ull << c) - 1);
     // high targets allowed per pass besides the always-present low bits
     const int highSlots = k - c;
+    const int n = (int)ops.size();
 
-    int begin = 0;
-    u64 cur = 0;
-    for (int i = 0; i < (int)ops.size(); i++) {
-        u64 tm = targetMask(ops[i]);
-        u64 merged = cur | tm;
-        bool fits = popcount64(merged & ~low) <= highSlots;
-        if (i > begin && (!fuse || !fits)) {
-            emitPass(ops, begin, i, cur, L, k, c, out);
-            begin = i;
-            cur = tm;
-        } else {
-            cur = merged;
-        }
+    if (!fuse) {
+        for (int i = 0; i < n; i++) emitPass(ops, i, i + 1, targetMask(ops[i]), L, k, c, out);
+        return;
     }
-    emitPass(ops, begin, (int)ops.size(), cur, L, k, c, out);
+
+    // List scheduling with commutation: a pass greedily collects every queued
+    // op whose targets fit the pass's tile bits and that commutes with all the
+    // earlier ops left for later passes.  Two ops commute when neither's
+    // targets meet the other's touched bits (controls and diagonal phase masks
+    // act diagonally, so they commute among themselves).  Diagonal ops need
+    // no tile bits at all.
+    std::vector<Op> order;
+    order.reserve(n);
+    std::vector<char> done(n, 0);
+    int first = 0;
+    while ((int)order.size() < n) {
+        while (done[first]) first++;
+        const int begin = (int)order.size();
+        u64 high = 0;           // high tile bits claimed by this pass
+        u64 blockedTg = 0;      // targets of ops deferred past this pass
+        u64 blockedTouch = 0;   // targets | controls of deferred ops
+        for (int i = first; i < n; i++) {
+            if (done[i]) continue;
+            const u64 tg = targetMask(ops[i]);
+            const u64 touch = tg | ops[i].ctrl;
+            const bool free = !(tg & blockedTouch) && !(touch & blockedTg);
+            const u64 need = high | (tg & ~low);
+            if (free && popcount64(need) <= highSlots) {
+                high = need;
+                order.push_back(ops[i]);
+                done[i] = 1;
+            } else {
+                blockedTg |= tg;
+                blockedTouch |= touch;
+            }
+        }
+        emitPass(order, begin, (int)order.size(), high, L, k, c, out);
+    }
+    ops.swap(order);
 }
 
 namespace {

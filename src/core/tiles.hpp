@@ -92,9 +92,10 @@ void planDenseBlocks(TileProgram& prog, int k, int R);
 void planPhases(TileProgram& prog, int k, int R);
 
 // Split `ops` (physical local positions, L local qubits) into passes of at
-// most kmax tile qubits (kmax >= cmin + 4).  With fuse=false every op gets its
-// own pass.
-void planTiles(const std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out);
+// most kmax tile qubits (kmax >= cmin + 4).  With fuse=true ops are reordered
+// where they commute to fill each pass (`ops` is left in execution order);
+// with fuse=false every op gets its own pass, in order.
+void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out);
 
 // Physical chunk index of element p of tile T in a pass.
 inline i64 tileBase(const TilePass& ps, i64 T, int L) {

@@ -26,8 +26,11 @@ hipDeviceProp_t g_prop;
 
 // Ring of pinned upload slots for tile programs; a slot is reused only after
 // the event recorded behind its last use has completed.
+// A slot holds the program of one flush: at most kMaxQueued ops, as many
+// phases and as many dense 2^R x 2^R blocks (every phase and block holds at
+// least one op).
 constexpr int kSlots = 32;
-constexpr size_t kSlotBytes = 128 << 10;
+constexpr size_t kSlotBytes = 1 << 20;
 char* g_progHost = nullptr;
 char* g_progDev = nullptr;
 hipEvent_t g_slotEvent[kSlots];
@@ -43,7 +46,7 @@ Tuning& tuning() {
             return e ? atoi(e) : d;
         };
         x.directKernels = env("QUEST_DIRECT_KERNELS", 1);
-        x.tileMode = env("QUEST_TILE_MODE", 2);
+        x.tileMode = env("QUEST_TILE_MODE", 0);
         x.tileWgPerCU = env("QUEST_TILE_WG_PER_CU", 2);
         return x;
     }();
@@ -68,6 +71,9 @@ using namespace hipk;
 namespace {
 
 constexpr size_t kMaxQueued = 256;
+static_assert(kMaxQueued * (sizeof(TileOp) + sizeof(TilePhase) + sizeof(real) * 2 * (1 << (2 * kRegSlots))) <=
+                  kSlotBytes,
+              "upload slot too small for a full flush");
 
 int tileQubits(int L) {
     const int cmin = sizeof(real) == 8 ? 4 : 5;

@@ -458,7 +458,7 @@ __device__ __forceinline__ typename Vec16<T>::type ldsGetVec(const T* s, unsigne
 // vectors per array for the HBM <-> LDS moves.
 // MODE 0: ops one by one on LDS; 1: register phases; 2: dense blocks
 template <typename T, int K, int MODE>
-__global__ __launch_bounds__(256) void tilePassKernelK(T* __restrict__ re, T* __restrict__ im, TileArgs a,
+__global__ __launch_bounds__(256, MODE == 1 ? 2 : 4) void tilePassKernelK(T* __restrict__ re, T* __restrict__ im, TileArgs a,
                                                        const TileOp* __restrict__ ops,
                                                        const TilePhase* __restrict__ phases,
                                                        const real* __restrict__ mats) {
@@ -501,32 +501,34 @@ __global__ __launch_bounds__(256) void tilePassKernelK(T* __restrict__ re, T* __
         return base;
     };
 
+    // Software pipeline, one tile ahead: the loads of tile i+1 are issued
+    // before the ops of tile i and are only consumed (register -> LDS) after
+    // the stores of tile i, in the same iteration, so the wait on them leaves
+    // those stores in flight.  The prefetch is branch-free (the last
+    // iteration re-reads its own tile) to keep the vmcnt accounting exact.
     V rr[U], ri[U];
     long long tile = blockIdx.x;
-    long long base = tile < a.numTiles ? tileBaseOf(tile) : 0;
-    if (tile < a.numTiles) {
+    if (tile >= a.numTiles) return;
+    long long base = tileBaseOf(tile);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            rr[u] = *reinterpret_cast<const V*>(re + base + off[u]);
-            ri[u] = *reinterpret_cast<const V*>(im + base + off[u]);
-        }
+    for (int u = 0; u < U; u++) {
+        rr[u] = *reinterpret_cast<const V*>(re + base + off[u]);
+        ri[u] = *reinterpret_cast<const V*>(im + base + off[u]);
     }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const unsigned p = (threadIdx.x + 256u * u) * VN;
+        ldsPutVec<T>(sre, p, rr[u]);
+        ldsPutVec<T>(sim, p, ri[u]);
+    }
+    __syncthreads();
     for (; tile < a.numTiles; tile += gridDim.x) {
+        const long long next = tile + gridDim.x;
+        const long long nbase = next < a.numTiles ? tileBaseOf(next) : base;
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const unsigned p = (threadIdx.x + 256u * u) * VN;
-            ldsPutVec<T>(sre, p, rr[u]);
-            ldsPutVec<T>(sim, p, ri[u]);
-        }
-        __syncthreads();
-        const long long next = tile + gridDim.x;
-        const long long nbase = next < a.numTiles ? tileBaseOf(next) : 0;
-        if (next < a.numTiles) {
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                rr[u] = *reinterpret_cast<const V*>(re + nbase + off[u]);
-                ri[u] = *reinterpret_cast<const V*>(im + nbase + off[u]);
-            }
+            rr[u] = *reinterpret_cast<const V*>(re + nbase + off[u]);
+            ri[u] = *reinterpret_cast<const V*>(im + nbase + off[u]);
         }
         if constexpr (PHASES) {
             for (int h = 0; h < a.nPhases; h++) {
@@ -559,6 +561,13 @@ __global__ __launch_bounds__(256) void tilePassKernelK(T* __restrict__ re, T* __
             const unsigned p = (threadIdx.x + 256u * u) * VN;
             *reinterpret_cast<V*>(re + base + off[u]) = ldsGetVec<T>(sre, p);
             *reinterpret_cast<V*>(im + base + off[u]) = ldsGetVec<T>(sim, p);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const unsigned p = (threadIdx.x + 256u * u) * VN;
+            ldsPutVec<T>(sre, p, rr[u]);
+            ldsPutVec<T>(sim, p, ri[u]);
         }
         __syncthreads();
         base = nbase;

@@ -26,7 +26,7 @@ int numCUs();
 // runtime knobs (env QUEST_* at start-up, setQuESTTuning() afterwards)
 struct Tuning {
     int directKernels = 1;  // LDS-free kernels for single-op passes
-    int tileMode = 2;       // fused tiles: 0 op by op, 1 register phases, 2 dense blocks
+    int tileMode = 0;       // fused tiles: 0 op by op (default), 1 register phases, 2 dense blocks
     int tileWgPerCU = 2;    // grid of the register-phase tile kernel, per CU
 };
 Tuning& tuning();

@@ -1,0 +1,87 @@
+"""Gate-fusion planner tests (CPU backend): the commutation-aware pass
+scheduler (src/core/tiles.cpp planTiles) may reorder queued ops; results
+must match the unfused oracle for every tile width, for state-vectors and
+density matrices with noise, and the pass count must stay low on layered
+circuits."""
+import math
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture
+def fuse_width():
+    from quest_amd.ops import capi
+
+    yield capi
+    capi.setFusionMaxQubits(0)
+    capi.setGateFusion(1)
+
+
+@pytest.mark.parametrize("width", [5, 6, 8, 10])
+@pytest.mark.parametrize("n", [9, 12])
+def test_random_ops_any_tile_width(env, fuse_width, width, n):
+    import quest_amd as qa
+    from helpers import apply_random_ops, assert_close, oracle_for
+
+    fuse_width.setFusionMaxQubits(width)
+    rng = np.random.default_rng(1000 * width + n)
+    reg = qa.Register(env, n)
+    o = oracle_for(reg, rng)
+    apply_random_ops(reg, o, rng, 300)
+    assert_close(reg, o)
+    reg.close()
+
+
+@pytest.mark.parametrize("width", [5, 7])
+def test_density_noise_reordered(env, fuse_width, width):
+    import quest_amd as qa
+    from helpers import apply_random_ops, assert_close, oracle_for
+
+    fuse_width.setFusionMaxQubits(width)
+    rng = np.random.default_rng(width)
+    reg = qa.Register(env, 5, density=True)
+    o = oracle_for(reg, rng)
+    apply_random_ops(reg, o, rng, 120, noise=True)
+    assert_close(reg, o, tol=1e-9)
+    reg.close()
+
+
+def test_collapse_between_gates_is_ordered(env, fuse_width):
+    """Collapse (a projector op) must not move across gates on its qubit."""
+    import quest_amd as qa
+
+    fuse_width.setFusionMaxQubits(6)
+    reg = qa.Register(env, 10)
+    reg.init_plus()
+    for q in range(10):
+        reg.h(q)          # back to |0...0>
+    reg.x(3)
+    assert reg.collapse(3, 1) == pytest.approx(1.0)
+    reg.h(3)
+    assert reg.prob(3, 0) == pytest.approx(0.5)
+    reg.close()
+
+
+def test_layered_circuit_pass_count(env, fuse_width):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.utils import oracle as O
+
+    n, depth = 18, 6
+    fuse_width.setFusionMaxQubits(10)
+    c = random_layered(n, depth, seed=3)
+    reg = qa.Register(env, n)
+    reg.init_plus()
+    reg.sync()
+    fuse_width.resetQuESTStats()
+    c.apply(reg)
+    reg.sync()
+    passes = fuse_width.getQuESTStats()["passes"]
+    # 14 high qubits over 6 free tile slots per pass: >= 3 passes per layer
+    # in program order; reordering across layers must do better than that
+    assert passes < 3 * depth, passes
+    o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
+    c.apply_oracle(o)
+    assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
+    reg.close()

@@ -99,6 +99,32 @@ def test_random_circuit_fused_and_eager(genv, n, fusion):
         qa.capi.setGateFusion(1)
 
 
+@pytest.mark.parametrize("tile_mode", [0, 1, 2])
+@pytest.mark.parametrize("direct", [0, 1])
+def test_long_queue_every_tile_mode(genv, tile_mode, direct):
+    """More ops than one flush holds (the queue flushes itself at 256) in
+    every fused-tile variant; state must match the oracle."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.utils import oracle as O
+
+    n = 18
+    assert qa.capi.setQuESTTuning("tile_mode", tile_mode) == 1
+    assert qa.capi.setQuESTTuning("direct_kernels", direct) == 1
+    try:
+        c = random_layered(n, 16, seed=tile_mode * 2 + direct)
+        reg = qa.Register(genv, n)
+        reg.init_plus()
+        c.apply(reg)
+        o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
+        c.apply_oracle(o)
+        assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
+        reg.close()
+    finally:
+        qa.capi.setQuESTTuning("tile_mode", 0)
+        qa.capi.setQuESTTuning("direct_kernels", 1)
+
+
 def test_reductions_and_collapse_large(genv):
     """24 qubits: 128 MiB per array; norm, per-qubit probabilities, inner
     product and collapse against quantities computed from the same state."""

@@ -21,7 +21,7 @@ VARIANTS = {
     "eager-direct": dict(fusion=0, tile_mode=2, direct_kernels=1),
     "eager-tile": dict(fusion=0, tile_mode=2, direct_kernels=0),
 }
-DEFAULTS = {"tile_mode": 2, "direct_kernels": 1, "tile_wg_per_cu": 2}
+DEFAULTS = {"tile_mode": 0, "direct_kernels": 1, "tile_wg_per_cu": 2}
 
 
 def main():
