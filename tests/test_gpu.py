@@ -218,3 +218,13 @@ def test_fp32_library_builds_and_loads():
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert out.returncode == 0, out.stderr
     assert "fp32 ok" in out.stdout
+
+
+def test_reference_golden_suite_on_gpu(genv):
+    """All golden cases of the reference's tests/**/*.test data on the HIP
+    backend (tests/test_reference_suite.py runs them on the CPU build)."""
+    from quest_amd.utils import golden
+
+    passed, failures = golden.run_all(genv.env)
+    assert not failures, "\n".join(failures[:20])
+    assert passed >= 770

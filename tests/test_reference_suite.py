@@ -1,0 +1,182 @@
+"""The reference's own test suite, run against this framework.
+
+* Golden data: all 773 cases of the reference's ``tests/**/*.test`` data files
+  (converted to ``tests/data/reference_golden.json``), run by
+  ``quest_amd.utils.golden`` in one process and over 2 and 4 ranks (CPU
+  socket transport: every 3-qubit register is spread over the ranks, so the
+  global-qubit exchange paths run; the reference's ``mpiexec -n 4`` strategy,
+  SURVEY.md §4.3).
+* The reference's Python-coded tests, re-written here with the same inputs
+  and expected values: essential/state_vector/{createQureg, createDensityQureg,
+  destroyQureg, seedQuEST}.test, unit/state_vector/maths/{calcFidelity,
+  calcInnerProduct, measure, measureWithStats}.test, algor/{QFT,
+  rotate_test}.test.  (The reference's QFTtests file holds placeholder data
+  that is not the QFT of |000>; the QFT is checked against the
+  NumPy oracle instead.)
+"""
+import math
+
+import numpy as np
+import pytest
+
+from quest_amd.ops import capi
+
+
+def test_golden_suite_single_process(env):
+    from quest_amd.utils import golden
+
+    passed, failures = golden.run_all(env.env)
+    assert not failures, "\n".join(failures[:20])
+    assert passed >= 770
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_golden_suite_distributed(ranks):
+    import os
+
+    from quest_amd.parallel import spawn_local
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = spawn_local(["-m", "quest_amd.utils.golden"], ranks,
+                      env_extra={"QUEST_BACKEND": "cpu", "PYTHONPATH": root}, timeout=600)
+    for r, p in enumerate(res):
+        assert p.returncode == 0, f"rank {r}:\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    assert " 0 failed" in res[0].stdout
+    assert int(res[0].stdout.strip().split()[-4]) >= 770
+
+
+# --- essential/state_vector ----------------------------------------------------------------
+
+def test_create_qureg_fields(env):
+    q = capi.createQureg(3, env.env)
+    assert not q.isDensityMatrix
+    assert q.numAmpsTotal == 8 and q.numQubitsInStateVec == 3 and q.numQubitsRepresented == 3
+    capi.destroyQureg(q, env.env)
+
+
+def test_create_density_qureg_fields(env):
+    q = capi.createDensityQureg(3, env.env)
+    assert q.isDensityMatrix
+    assert q.numAmpsTotal == 64 and q.numQubitsInStateVec == 6 and q.numQubitsRepresented == 3
+    capi.destroyQureg(q, env.env)
+
+
+def test_destroy_qureg(env):
+    q = capi.createQureg(3, env.env)
+    capi.destroyQureg(q, env.env)
+
+
+def test_seed_quest_mt19937_golden(env):
+    capi.seedQuEST([(3 * i) % 64 for i in range(64)], 64)
+    expect = [0.3388381249594591, 0.9577616744110737, 0.30208554964095485, 0.008018929047514434,
+              0.6887747446747438]
+    got = [capi.genrand_real1() for _ in range(5)]
+    assert got == pytest.approx(expect, abs=1e-15)
+
+
+# --- unit/state_vector/maths (Python-coded) --------------------------------------------------
+
+def test_calc_fidelity(env):
+    a, b = capi.createQureg(3, env.env), capi.createQureg(3, env.env)
+    assert capi.calcFidelity(a, b) == pytest.approx(1.0, abs=1e-10)
+    capi.initPlusState(a)
+    assert capi.calcFidelity(a, b) == pytest.approx(0.125, abs=1e-10)
+    capi.initStateDebug(a)
+    assert capi.calcFidelity(a, b) == pytest.approx(0.01, abs=1e-10)
+    capi.destroyQureg(a, env.env)
+    capi.destroyQureg(b, env.env)
+
+
+def test_calc_inner_product(env):
+    a, b = capi.createQureg(3, env.env), capi.createQureg(3, env.env)
+    assert abs(capi.calcInnerProduct(a, b) - 1) < 1e-10
+    capi.initPlusState(a)
+    assert abs(capi.calcInnerProduct(a, b) - 0.3535533905933) < 1e-10
+    capi.initStateDebug(a)
+    assert abs(capi.calcInnerProduct(a, b) - (-0.1j)) < 1e-10
+    capi.destroyQureg(a, env.env)
+    capi.destroyQureg(b, env.env)
+
+
+def test_measure_seeded(env):
+    q = capi.createQureg(3, env.env)
+    capi.initZeroState(q)
+    capi.seedQuEST([1], 1)
+    assert [capi.measure(q, i) for i in range(3)] == [0, 0, 0]
+    capi.initPlusState(q)
+    assert [capi.measure(q, i) for i in range(3)] == [0, 1, 1]
+    capi.initStateDebug(q)
+    assert [capi.measure(q, i) for i in range(3)] == [0, 1, 1]
+    capi.destroyQureg(q, env.env)
+
+
+def test_measure_with_stats_seeded(env):
+    q = capi.createQureg(3, env.env)
+    capi.seedQuEST([1], 1)
+    capi.initZeroState(q)
+    assert [capi.measureWithStats(q, i)[1] for i in range(3)] == pytest.approx([1.0] * 3, abs=1e-10)
+    capi.initPlusState(q)
+    assert [capi.measureWithStats(q, i)[1] for i in range(3)] == pytest.approx([0.5] * 3, abs=1e-10)
+    capi.initStateDebug(q)
+    assert [capi.measureWithStats(q, i)[1] for i in range(3)] == pytest.approx(
+        [5.0, 0.708, 0.884180790960452], abs=1e-10)
+    capi.destroyQureg(q, env.env)
+
+
+# --- algor ----------------------------------------------------------------------------------
+
+def _qft(q, n):
+    for qubit in range(n):
+        capi.hadamard(q, qubit)
+        angle = math.pi
+        for actor in range(qubit + 1, n):
+            angle /= 2.0
+            capi.controlledPhaseShift(q, actor, qubit, angle)
+
+
+def test_qft_forward_and_again(env):
+    from quest_amd.utils import oracle as O
+
+    n = 3
+    q = capi.createQureg(n, env.env)
+    capi.initZeroState(q)
+    o = O.StateVector(n)
+    for rep in range(2):
+        _qft(q, n)
+        for qubit in range(n):
+            o.apply(O.H, qubit)
+            angle = math.pi
+            for actor in range(qubit + 1, n):
+                angle /= 2.0
+                o.apply(np.diag([1, np.exp(1j * angle)]), qubit, controls=[actor])
+        got = capi.getAmps(q)
+        assert np.max(np.abs(got - o.v)) < 1e-10
+        if rep == 0:
+            assert np.allclose(np.abs(got), 1 / math.sqrt(8))
+    capi.destroyQureg(q, env.env)
+
+
+def test_rotate_round_trip_and_normalisation(env):
+    angs = [1.2, -2.4, 0.3]
+    alpha = complex(math.cos(angs[0]) * math.cos(angs[1]), math.cos(angs[0]) * math.sin(angs[1]))
+    beta = complex(math.sin(angs[0]) * math.cos(angs[2]), math.sin(angs[0]) * math.sin(angs[2]))
+    n = 10
+    mq, ver = capi.createQureg(n, env.env), capi.createQureg(n, env.env)
+    capi.initStateDebug(mq)
+    capi.initStateDebug(ver)
+    for t in range(n):
+        capi.compactUnitary(mq, t, alpha, beta)
+    assert not capi.compareStates(mq, ver, 1e-10)
+    alpha_b, beta_b = alpha.conjugate(), -beta
+    for t in range(n):
+        capi.compactUnitary(mq, t, alpha_b, beta_b)
+    assert capi.compareStates(mq, ver, 1e-9)
+    capi.destroyQureg(mq, env.env)
+    capi.destroyQureg(ver, env.env)
+    n = 25 if capi.getQuESTBackend() == "HIP" else 20
+    mq = capi.createQureg(n, env.env)
+    capi.initPlusState(mq)
+    for t in range(n):
+        capi.compactUnitary(mq, t, alpha_b, beta_b)
+    assert capi.calcTotalProb(mq) == pytest.approx(1.0, abs=1e-10)
+    capi.destroyQureg(mq, env.env)
