@@ -19,8 +19,8 @@ JOBS      ?= 8
 
 COMMON_SRC := src/api/api.cpp src/api/validation.cpp src/api/qasm.cpp src/api/common.cpp \
               src/api/mt19937.cpp src/core/router.cpp src/core/tiles.cpp src/comm/bootstrap.cpp
-CPU_SRC    := $(COMMON_SRC) src/comm/comm_socket.cpp src/cpu/backend_cpu.cpp
-HIP_HOST   := $(COMMON_SRC) src/comm/comm_rccl.cpp
+CPU_SRC    := $(COMMON_SRC) src/comm/comm_socket.cpp src/comm/comm_host.cpp src/cpu/backend_cpu.cpp
+HIP_HOST   := $(COMMON_SRC) src/comm/comm_socket.cpp src/comm/comm_rccl.cpp
 HIP_DEV    := src/hip/backend_hip.hip src/hip/kernels_gates.hip src/hip/kernels_direct.hip src/hip/kernels_reduce.hip src/hip/kernels_misc.hip
 
 INCLUDES   := -Iinclude

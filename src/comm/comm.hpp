@@ -6,7 +6,10 @@
 //   HIP build  -> RCCL (comm_rccl.cpp): pairwise ncclSend/ncclRecv over the
 //                 direct xGMI link, ncclAllReduce / ncclBroadcast, all ordered
 //                 on the backend's HIP stream (no host round trip per slice);
-//   CPU build  -> TCP sockets (comm_socket.cpp), used for multi-process tests.
+//   CPU build  -> TCP sockets (comm_socket.cpp), used for multi-process tests;
+//   HIP build with QUEST_COMM=socket -> the same sockets with device buffers
+//                 staged through pinned host memory (several ranks on one GPU,
+//                 for tests; RCCL needs one GPU per rank).
 // Both are bootstrapped by bootstrap.cpp from torchrun-style environment
 // variables (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT) or
 // QUEST_BOOTSTRAP_ADDR / QUEST_BOOTSTRAP_PORT.
@@ -40,6 +43,16 @@ void barrier();
 std::string describe();
 
 }  // namespace comm
+
+// ---- TCP socket mesh on host buffers (comm_socket.cpp) ------------------------
+namespace sock {
+void init(int rank, int size);
+void finalize();
+void sendrecv(int peer, const void* send, void* recv, size_t bytes);
+void allreduceSum(double* vals, int n);
+void bcastHost(void* buf, size_t bytes, int root);
+void allgatherHost(const void* send, void* recv, size_t bytesPerRank);
+}  // namespace sock
 
 // ---- bootstrap (bootstrap.cpp) ----------------------------------------------
 namespace boot {

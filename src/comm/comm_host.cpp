@@ -1,0 +1,37 @@
+// comm:: for the host (CPU) build: the socket mesh of comm_socket.cpp on
+// host buffers (the state lives in host memory).
+#include "comm.hpp"
+
+namespace qa {
+namespace comm {
+
+namespace {
+int g_size = 1;
+}
+
+void init(int rank, int size) {
+    g_size = size;
+    sock::init(rank, size);
+}
+void finalize() {
+    sock::finalize();
+    g_size = 1;
+}
+bool active() { return g_size > 1; }
+void sendrecv(int peer, const void* send, void* recv, size_t bytes) { sock::sendrecv(peer, send, recv, bytes); }
+void allreduceSum(double* vals, int n) { sock::allreduceSum(vals, n); }
+int allreduceAnd(int v) {
+    double d = v ? 0.0 : 1.0;  // count failures
+    sock::allreduceSum(&d, 1);
+    return d == 0.0 ? 1 : 0;
+}
+void bcastHost(void* buf, size_t bytes, int root) { sock::bcastHost(buf, bytes, root); }
+void allgather(const void* send, void* recv, size_t bytesPerRank) { sock::allgatherHost(send, recv, bytesPerRank); }
+void barrier() {
+    double d = 1;
+    sock::allreduceSum(&d, 1);
+}
+std::string describe() { return g_size > 1 ? "TCP socket mesh (host build)" : "single process"; }
+
+}  // namespace comm
+}  // namespace qa

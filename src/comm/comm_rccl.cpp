@@ -12,6 +12,10 @@
 // librccl is loaded with dlopen: inside a Python process that already loaded
 // PyTorch we bind to torch's RCCL (same HIP runtime); standalone C programs
 // get /opt/rocm's.
+//
+// QUEST_COMM=socket selects the test transport instead: the TCP socket mesh
+// of comm_socket.cpp with every device buffer staged through pinned host
+// memory, so that several ranks can share one GPU (RCCL refuses that).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -47,6 +51,9 @@ struct Rccl {
 } R;
 
 int g_rank = 0, g_size = 1;
+bool g_socket = false;          // QUEST_COMM=socket test transport
+char* g_stage = nullptr;        // pinned staging for the socket transport
+size_t g_stageBytes = 0;
 ncclComm_t g_comm = nullptr;
 double* g_dScalars = nullptr;   // device scratch for scalar collectives
 double* g_hScalars = nullptr;   // pinned host mirror
@@ -103,12 +110,28 @@ void loadRccl() {
 
 hipStream_t S() { return hipk::stream(); }
 
+// pinned host staging of at least `bytes` (socket transport)
+char* stage(size_t bytes) {
+    if (bytes > g_stageBytes) {
+        if (g_stage) QA_HIP_CHECK(hipHostFree(g_stage));
+        g_stageBytes = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
+        QA_HIP_CHECK(hipHostMalloc(&g_stage, g_stageBytes, hipHostMallocDefault));
+    }
+    return g_stage;
+}
+
 }  // namespace
 
 void init(int rank, int size) {
     g_rank = rank;
     g_size = size;
     if (size == 1) return;
+    const char* mode = getenv("QUEST_COMM");
+    g_socket = mode && !strcmp(mode, "socket");
+    if (g_socket) {
+        sock::init(rank, size);
+        return;
+    }
     loadRccl();
     ncclUniqueId id;
     memset(&id, 0, sizeof id);
@@ -122,6 +145,13 @@ void init(int rank, int size) {
 }
 
 void finalize() {
+    if (g_socket) {
+        sock::finalize();
+        if (g_stage) (void)hipHostFree(g_stage);
+        g_stage = nullptr;
+        g_stageBytes = 0;
+        g_socket = false;
+    }
     if (g_comm) {
         QA_HIP_CHECK(hipStreamSynchronize(S()));
         R.commDestroy(g_comm);
@@ -140,6 +170,15 @@ void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
         QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, S()));
         return;
     }
+    if (g_socket) {
+        char* h = stage(2 * bytes);
+        QA_HIP_CHECK(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, S()));
+        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        sock::sendrecv(peer, h, h + bytes, bytes);
+        QA_HIP_CHECK(hipMemcpyAsync(recv, h + bytes, bytes, hipMemcpyHostToDevice, S()));
+        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        return;
+    }
     QA_NCCL(R.groupStart(), "ncclGroupStart");
     QA_NCCL(R.send(send, bytes, ncclUint8, peer, g_comm, S()), "ncclSend");
     QA_NCCL(R.recv(recv, bytes, ncclUint8, peer, g_comm, S()), "ncclRecv");
@@ -148,6 +187,10 @@ void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
 
 void allreduceSum(double* vals, int n) {
     if (g_size == 1) return;
+    if (g_socket) {
+        sock::allreduceSum(vals, n);
+        return;
+    }
     for (int off = 0; off < n; off += 64) {
         int k = n - off < 64 ? n - off : 64;
         memcpy(g_hScalars, vals + off, sizeof(double) * k);
@@ -167,6 +210,10 @@ int allreduceAnd(int v) {
 
 void bcastHost(void* buf, size_t bytes, int root) {
     if (g_size == 1) return;
+    if (g_socket) {
+        sock::bcastHost(buf, bytes, root);
+        return;
+    }
     char* p = (char*)buf;
     const size_t cap = sizeof(double) * 64;
     for (size_t off = 0; off < bytes; off += cap) {
@@ -185,6 +232,16 @@ void allgather(const void* send, void* recv, size_t bytesPerRank) {
         QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytesPerRank, hipMemcpyDeviceToDevice, S()));
         return;
     }
+    if (g_socket) {
+        const size_t all = bytesPerRank * (size_t)g_size;
+        char* h = stage(bytesPerRank + all);
+        QA_HIP_CHECK(hipMemcpyAsync(h, send, bytesPerRank, hipMemcpyDeviceToHost, S()));
+        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        sock::allgatherHost(h, h + bytesPerRank, bytesPerRank);
+        QA_HIP_CHECK(hipMemcpyAsync(recv, h + bytesPerRank, all, hipMemcpyHostToDevice, S()));
+        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        return;
+    }
     QA_NCCL(R.allGather(send, recv, bytesPerRank, ncclUint8, g_comm, S()), "ncclAllGather");
 }
 
@@ -195,6 +252,7 @@ void barrier() {
 
 std::string describe() {
     if (g_size == 1) return "single process";
+    if (g_socket) return "TCP socket mesh, device buffers staged through host (QUEST_COMM=socket)";
     int v = 0;
     if (R.getVersion) R.getVersion(&v);
     char buf[256];

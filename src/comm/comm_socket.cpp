@@ -1,8 +1,10 @@
-// TCP-socket transport for the host (CPU) build: a full mesh of sockets
-// between ranks, used for multi-process tests of the distributed router on
-// machines without GPUs (the analogue of the reference's oversubscribed
-// `mpiexec -n 4` test runs).  Same interface as the RCCL
-// transport; buffers are host memory.
+// TCP-socket transport: a full mesh of sockets between ranks on host
+// buffers.  The CPU build's only transport (comm_host.cpp), and in the HIP
+// build the test transport selected by QUEST_COMM=socket (comm_rccl.cpp stages
+// device buffers through pinned host memory), which lets several ranks share
+// ONE GPU -- RCCL refuses two ranks on a device -- so the distributed router
+// and its GPU kernels are tested on a single-GPU box (the analogue of the
+// reference's oversubscribed `mpiexec -n 4` runs).
 #include "comm.hpp"
 
 #include <arpa/inet.h>
@@ -21,7 +23,7 @@
 #include <vector>
 
 namespace qa {
-namespace comm {
+namespace sock {
 
 namespace {
 int g_rank = 0, g_size = 1;
@@ -156,8 +158,6 @@ void finalize() {
     g_size = 1;
 }
 
-bool active() { return g_size > 1; }
-
 void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
     if (peer == g_rank) {
         memcpy(recv, send, bytes);
@@ -181,12 +181,6 @@ void allreduceSum(double* vals, int n) {
     }
 }
 
-int allreduceAnd(int v) {
-    double d = v ? 0.0 : 1.0;  // count failures
-    allreduceSum(&d, 1);
-    return d == 0.0 ? 1 : 0;
-}
-
 void bcastHost(void* buf, size_t bytes, int root) {
     if (g_size == 1) return;
     if (g_rank == root) {
@@ -197,20 +191,11 @@ void bcastHost(void* buf, size_t bytes, int root) {
     }
 }
 
-void allgather(const void* send, void* recv, size_t bytesPerRank) {
+void allgatherHost(const void* send, void* recv, size_t bytesPerRank) {
     char* out = (char*)recv;
     memcpy(out + (size_t)g_rank * bytesPerRank, send, bytesPerRank);
     for (int r = 0; r < g_size; r++) bcastHost(out + (size_t)r * bytesPerRank, bytesPerRank, r);
 }
 
-void barrier() {
-    double d = 1;
-    allreduceSum(&d, 1);
-}
-
-std::string describe() {
-    return g_size > 1 ? "TCP socket mesh (host build)" : "single process";
-}
-
-}  // namespace comm
+}  // namespace sock
 }  // namespace qa

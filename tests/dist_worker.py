@@ -1,0 +1,26 @@
+"""One rank of a distributed-equivalence run:
+``python tests/dist_worker.py <scenario> <out.npz>`` (rank 0 writes)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import quest_amd as qa
+    from scenarios import SCENARIOS
+
+    name, out = sys.argv[1], sys.argv[2]
+    env = qa.Env()
+    res = SCENARIOS[name](env)
+    res["_ranks"] = env.num_ranks
+    if env.rank == 0:
+        import numpy as np
+
+        np.savez(out, **{k: np.asarray(v) for k, v in res.items()})
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

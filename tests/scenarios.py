@@ -1,0 +1,131 @@
+"""Deterministic workloads whose results must not depend on how many ranks
+run them (distributed-equivalence tests).  Each
+scenario takes an ``Env`` and returns a dict of numpy arrays / numbers,
+identical on every rank."""
+from __future__ import annotations
+
+import numpy as np
+
+from helpers import apply_random_noise, apply_random_ops
+
+
+class NullOracle:
+    """Stands in for the oracle in helpers.apply_* (only the register runs)."""
+
+    def __getattr__(self, name):
+        return lambda *a, **k: None
+
+
+def random_ops_statevector(env):
+    import quest_amd as qa
+
+    rng = np.random.default_rng(7)
+    r = qa.Register(env, 10)
+    r.init_plus()
+    apply_random_ops(r, NullOracle(), rng, 300)
+    out = {"state": r.to_numpy(), "probs": np.array([r.prob(q, 1) for q in range(10)]),
+           "norm": r.total_prob()}
+    r.close()
+    return out
+
+
+def random_ops_density(env):
+    import quest_amd as qa
+
+    rng = np.random.default_rng(8)
+    r = qa.Register(env, 5, density=True)
+    r.init_plus()
+    apply_random_ops(r, NullOracle(), rng, 80, noise=True)
+    for _ in range(10):
+        apply_random_noise(r, NullOracle(), rng)
+    out = {"state": r.to_numpy(), "purity": r.purity(), "trace": r.total_prob(),
+           "probs": np.array([r.prob(q, 0) for q in range(5)])}
+    r.close()
+    return out
+
+
+def measurement_and_collapse(env):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    r = qa.Register(env, 12)
+    r.init_plus()
+    random_layered(12, 4, seed=3).apply(r)
+    capi.seedQuEST([11, 22, 33], 3)
+    outcomes = [r.measure(q) for q in (11, 0, 6, 3)]
+    p = r.collapse(9, 1) if r.prob(9, 1) > 1e-6 else r.collapse(9, 0)
+    ms = [r.measure_with_stats(q) for q in (1, 10)]
+    out = {"outcomes": np.array(outcomes), "p": p, "ms": np.array(ms, dtype=float), "state": r.to_numpy()}
+    d = qa.Register(env, 4, density=True)
+    d.init_plus()
+    d.h(3)
+    d.cnot(3, 0)
+    d.damping(0, 0.3)
+    out["dens_outcomes"] = np.array([d.measure(q) for q in (0, 3, 2)])
+    out["dens_state"] = d.to_numpy()
+    r.close()
+    d.close()
+    return out
+
+
+def calculations(env):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    n = 9
+    a, b = qa.Register(env, n), qa.Register(env, n)
+    a.init_plus()
+    random_layered(n, 3, seed=1).apply(a)
+    b.init_classical(37)
+    b.h(8)
+    b.crx(8, 2, 0.7)
+    out = {"inner": a.inner(b), "fid": a.fidelity(b), "amp": a.amp(300), "amp0": b.amp(37)}
+    c = qa.Register(env, n)
+    c.clone_from(a)
+    c.ry(7, 0.4)
+    out["clone_inner"] = c.inner(a)
+    # density: initPureState, addDensityMatrix, fidelity vs pure, purity
+    d1, d2 = qa.Register(env, 4, density=True), qa.Register(env, 4, density=True)
+    p = qa.Register(env, 4)
+    p.init_plus()
+    p.rx(2, 1.1)
+    p.cnot(2, 3)
+    d1.init_pure(p)
+    d2.init_classical(5)
+    capi.addDensityMatrix(d1.q, 0.3, d2.q)
+    out["dfid"] = d1.fidelity(p)
+    out["dpur"] = d1.purity()
+    out["dstate"] = d1.to_numpy()
+    out["damp"] = d1.density_amp(5, 5)
+    # setAmps across the rank boundary + getAmp
+    e = qa.Register(env, 6)
+    e.init_zero()
+    vals = np.arange(20) * (0.01 + 0.02j)
+    capi.setAmps(e.q, 22, vals.real, vals.imag, 20)
+    out["setamps"] = e.to_numpy()
+    capi.initStateOfSingleQubit(e.q, 4, 1)
+    out["single"] = e.to_numpy()
+    for r in (a, b, c, d1, d2, p, e):
+        r.close()
+    return out
+
+
+def qasm_log(env):
+    import quest_amd as qa
+
+    r = qa.Register(env, 6)
+    r.start_qasm()
+    r.h(5)
+    r.cnot(5, 0)
+    r.crz(1, 4, 0.25)
+    r.mcz([0, 2, 5])
+    r.measure(5)
+    text = r.qasm
+    r.close()
+    return {"qasm": text}
+
+
+SCENARIOS = {f.__name__: f for f in (random_ops_statevector, random_ops_density, measurement_and_collapse,
+                                     calculations, qasm_log)}

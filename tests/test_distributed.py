@@ -1,0 +1,49 @@
+"""Distributed equivalence: the same workloads on 1
+rank (in process) and on 2 / 4 ranks (one process per rank, CPU socket
+transport, 127.0.0.1) must agree — state vectors, density matrices,
+probabilities, seeded measurement outcomes, reductions and QASM text.  The
+registers are small (6-12 qubits), so 1-2 of their qubits are global and
+every gate kind crosses the rank boundary (global<->local swaps, control
+bits on rank bits, chunk-level collapse)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+
+
+def _single(name, env):
+    from scenarios import SCENARIOS
+
+    return SCENARIOS[name](env)
+
+
+def _multi(name, ranks, tmp_path):
+    from quest_amd.parallel import spawn_local
+
+    out = str(tmp_path / f"{name}_{ranks}.npz")
+    res = spawn_local([os.path.join(HERE, "dist_worker.py"), name, out], ranks,
+                      env_extra={"QUEST_BACKEND": "cpu", "PYTHONPATH": ROOT}, timeout=600)
+    for r, p in enumerate(res):
+        assert p.returncode == 0, f"rank {r}:\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
+    with np.load(out, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+@pytest.mark.parametrize("name", ["random_ops_statevector", "random_ops_density", "measurement_and_collapse",
+                                  "calculations", "qasm_log"])
+def test_distributed_equivalence(env, tmp_path, name, ranks):
+    want = _single(name, env)
+    got = _multi(name, ranks, tmp_path)
+    assert int(got["_ranks"]) == ranks
+    for k, v in want.items():
+        g = got[k]
+        if isinstance(v, str):
+            assert str(g) == v, k
+        else:
+            np.testing.assert_allclose(np.asarray(g), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)

@@ -228,3 +228,35 @@ def test_reference_golden_suite_on_gpu(genv):
     passed, failures = golden.run_all(genv.env)
     assert not failures, "\n".join(failures[:20])
     assert passed >= 770
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+@pytest.mark.parametrize("name", ["random_ops_statevector", "random_ops_density", "measurement_and_collapse",
+                                  "calculations", "qasm_log"])
+def test_distributed_equivalence_on_gpu(genv, tmp_path, name, ranks):
+    """The distributed router with the HIP kernels (pack/unpack, chunk
+    predicates, reductions + allreduce) on ONE GPU shared by 2 / 4 ranks over
+    the QUEST_COMM=socket test transport, against the single-rank HIP run."""
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from scenarios import SCENARIOS
+
+    from quest_amd.parallel import spawn_local
+
+    want = SCENARIOS[name](genv)
+    out = str(tmp_path / f"{name}_{ranks}.npz")
+    res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks,
+                      env_extra={"QUEST_BACKEND": "hip", "QUEST_COMM": "socket",
+                                 "PYTHONPATH": os.path.dirname(here)}, timeout=600)
+    for r, p in enumerate(res):
+        assert p.returncode == 0, f"rank {r}:\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
+    with np.load(out, allow_pickle=False) as z:
+        got = {k: z[k] for k in z.files}
+    assert int(got["_ranks"]) == ranks
+    for k, v in want.items():
+        if isinstance(v, str):
+            assert str(got[k]) == v, k
+        else:
+            np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
