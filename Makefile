@@ -3,7 +3,8 @@
 #   make            -> CPU (host) libraries, fp64 + fp32   (no GPU needed)
 #   make hip        -> HIP libraries for gfx950, fp64 + fp32 (hipcc cross-compiles)
 #   make all        -> both
-#   make examples   -> C examples linked against the fp64 libraries
+#   make examples   -> C examples linked against the fp64 CPU library
+#   make examples-hip -> the same linked against the fp64 HIP library
 #
 # Outputs go to quest_amd/lib/ so they travel with the repository snapshot:
 #   libQuEST_cpu_f64.so  libQuEST_cpu_f32.so  libQuEST_hip_f64.so  libQuEST_hip_f32.so
@@ -29,7 +30,7 @@ HIPFLAGS   := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-func
               -Wno-unused-result -munsafe-fp-atomics $(INCLUDES)
 HIPHOST    := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $(INCLUDES) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 
-.PHONY: cpu hip all clean examples
+.PHONY: cpu hip all clean examples examples-hip
 
 cpu: $(LIBDIR)/libQuEST_cpu_f64.so $(LIBDIR)/libQuEST_cpu_f32.so
 hip: $(LIBDIR)/libQuEST_hip_f64.so $(LIBDIR)/libQuEST_hip_f32.so $(LIBDIR)/libQuEST.so
@@ -39,11 +40,11 @@ all: cpu hip
 define cpu_rules
 $(BUILD)/cpu_f$(2)/%.o: %.cpp $(wildcard include/*.h src/*/*.hpp)
 	@mkdir -p $$(dir $$@)
-	$(CXX) $(CXXFLAGS) -DQuEST_PREC=$(1) -c $$< -o $$@
+	$(CXX) $(CXXFLAGS) -fopenmp -DQuEST_PREC=$(1) -c $$< -o $$@
 
 $(LIBDIR)/libQuEST_cpu_f$(2).so: $(patsubst %.cpp,$(BUILD)/cpu_f$(2)/%.o,$(CPU_SRC))
 	@mkdir -p $(LIBDIR)
-	$(CXX) -shared -Wl,-Bsymbolic -o $$@ $$^ -lpthread
+	$(CXX) -shared -fopenmp -Wl,-Bsymbolic -o $$@ $$^ -lpthread
 endef
 $(eval $(call cpu_rules,2,64))
 $(eval $(call cpu_rules,1,32))
@@ -71,6 +72,7 @@ $(LIBDIR)/libQuEST.so: $(LIBDIR)/libQuEST_hip_f64.so
 # ---------------------------------------------------------------- examples
 EXAMPLES := tutorial_example damping_example bernstein_vazirani_circuit random_circuit_benchmark
 examples: $(addprefix $(BUILD)/examples/,$(addsuffix _cpu,$(EXAMPLES)))
+examples-hip: $(addprefix $(BUILD)/examples/,$(addsuffix _hip,$(EXAMPLES)))
 
 $(BUILD)/examples/%_cpu: examples/%.c $(LIBDIR)/libQuEST_cpu_f64.so
 	@mkdir -p $(dir $@)

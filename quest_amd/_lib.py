@@ -45,6 +45,9 @@ def resolve(backend: str | None = None, prec: int | None = None) -> tuple[str, i
     if backend not in ("hip", "cpu"):
         raise ValueError(f"unknown QUEST_BACKEND {backend!r}")
     name = f"libQuEST_{backend}_f{64 if prec == 2 else 32}.so"
+    override = os.environ.get("QUEST_LIB")  # e.g. a CMake build's library
+    if override:
+        return backend, prec, override
     return backend, prec, os.path.join(LIB_DIR, name)
 
 

@@ -4,6 +4,8 @@ from .circuits import (  # noqa: F401
     Gate,
     bernstein_vazirani,
     fork_benchmark,
+    fork_circuit,
+    load_api_circuit,
     ghz,
     qft,
     random_layered,

@@ -3,15 +3,18 @@ generators for the workloads the reference ships or benchmarks.
 
 * :func:`random_layered` - depth-D random circuit: a random single-qubit gate
   on every qubit, then a CNOT brick layer (the bench.py workload);
-* :func:`fork_benchmark` - the zhaozzz-160 fork's 30-qubit benchmark shape
-  (tutorial_example.c:29-534: 490 gates with the same gate-type histogram,
-  30 calcProbOfOutcome, 10 getAmp), regenerated with a seeded RNG;
+* :func:`fork_circuit` - the zhaozzz-160 fork's exact 30-qubit benchmark
+  circuit (tutorial_example.c:29-518, 490 gates; the program then takes 30
+  calcProbOfOutcome and 10 getAmp), read from examples/data;
+* :func:`fork_benchmark` - a seeded random circuit with the same gate-type
+  histogram, for other qubit counts;
 * :func:`qft`, :func:`ghz`, :func:`bernstein_vazirani` - the algorithms of the
   reference's tests/algor and examples/bernstein_vazirani_circuit.c.
 """
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -142,6 +145,44 @@ def fork_benchmark(seed: int = 2024, n: int = 30) -> Circuit:
         else:
             c.add(name, rng.integers(n))
     return c
+
+
+_API_TO_GATE = {
+    "hadamard": "h", "pauliX": "x", "pauliY": "y", "pauliZ": "z", "sGate": "s", "tGate": "t",
+    "rotateX": "rx", "rotateY": "ry", "rotateZ": "rz", "controlledNot": "cnot", "controlledPauliY": "cy",
+    "controlledRotateX": "crx", "controlledRotateY": "cry", "controlledRotateZ": "crz",
+    "controlledPhaseFlip": "cz", "phaseShift": "phase", "controlledPhaseShift": "cphase",
+}
+
+
+def load_api_circuit(path: str, n: int) -> Circuit:
+    """Read a text circuit of QuEST API calls, one per line:
+    ``<function> <qubits...> [<angle>]`` (examples/data/*.txt)."""
+    c = Circuit(n)
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            name, *args = line.split()
+            g = _API_TO_GATE[name]
+            if g in ("rx", "ry", "rz", "phase"):
+                c.add(g, int(args[0]), param=float(args[1]))
+            elif g in ("crx", "cry", "crz", "cphase"):
+                c.add(g, int(args[0]), int(args[1]), param=float(args[2]))
+            else:
+                c.add(g, *[int(a) for a in args])
+    return c
+
+
+FORK_CIRCUIT_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                 "examples", "data", "fork_circuit_30q.txt")
+
+
+def fork_circuit() -> Circuit:
+    """The fork's exact 30-qubit benchmark circuit (490 gates,
+    tutorial_example.c:29-518; extracted by tools/import_fork_circuit.py)."""
+    return load_api_circuit(FORK_CIRCUIT_FILE, 30)
 
 
 def qft(n: int) -> Circuit:

@@ -268,32 +268,41 @@ void runPhase(const TilePhase& ph, const TileProgram& prog, int k, i64 base, rea
     }
 }
 
+// OpenMP over tiles (each thread stages its own tile), as the reference's
+// CPU kernels parallelise their pair loops (QuEST_cpu.c, `#pragma omp
+// parallel for`); small registers stay on one thread.
+constexpr i64 kOmpMin = (i64)1 << 15;
+
 void runProgram(QuregImpl& q, const TileProgram& prog) {
     for (const TilePass& ps : prog.passes) {
         const unsigned n = 1u << ps.k;
         std::vector<i64> offs(n);
         for (unsigned p = 0; p < n; p++) offs[p] = tileOffset(ps, p);
-        std::vector<real> br(n), bi(n);
         const i64 tiles = (i64)1 << (q.L - ps.k);
-        for (i64 T = 0; T < tiles; T++) {
-            const i64 base = tileBase(ps, T, q.L);
-            for (unsigned p = 0; p < n; p++) {
-                br[p] = q.re[base + offs[p]];
-                bi[p] = q.im[base + offs[p]];
-            }
-            if (ps.phaseEnd > ps.phaseBegin) {
-                for (int h = ps.phaseBegin; h < ps.phaseEnd; h++)
-                    runPhase(prog.phases[h], prog, ps.k, base, br.data(), bi.data());
-            } else {
-                for (int o = ps.opBegin; o < ps.opEnd; o++) {
-                    const TileOp& op = prog.ops[o];
-                    if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
-                    applyTileOp(op, ps.k, br.data(), bi.data());
+#pragma omp parallel if (q.numAmpsPerChunk >= kOmpMin)
+        {
+            std::vector<real> br(n), bi(n);
+#pragma omp for schedule(static)
+            for (i64 T = 0; T < tiles; T++) {
+                const i64 base = tileBase(ps, T, q.L);
+                for (unsigned p = 0; p < n; p++) {
+                    br[p] = q.re[base + offs[p]];
+                    bi[p] = q.im[base + offs[p]];
                 }
-            }
-            for (unsigned p = 0; p < n; p++) {
-                q.re[base + offs[p]] = br[p];
-                q.im[base + offs[p]] = bi[p];
+                if (ps.phaseEnd > ps.phaseBegin) {
+                    for (int h = ps.phaseBegin; h < ps.phaseEnd; h++)
+                        runPhase(prog.phases[h], prog, ps.k, base, br.data(), bi.data());
+                } else {
+                    for (int o = ps.opBegin; o < ps.opEnd; o++) {
+                        const TileOp& op = prog.ops[o];
+                        if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
+                        applyTileOp(op, ps.k, br.data(), bi.data());
+                    }
+                }
+                for (unsigned p = 0; p < n; p++) {
+                    q.re[base + offs[p]] = br[p];
+                    q.im[base + offs[p]] = bi[p];
+                }
             }
         }
         stats().passes++;
@@ -359,6 +368,7 @@ void flush(QuregImpl& q) {
 
 void fill(QuregImpl& q, real re, real im) {
     flush(q);
+#pragma omp parallel for if (q.numAmpsPerChunk >= kOmpMin)
     for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
         q.re[i] = re;
         q.im[i] = im;
@@ -373,6 +383,7 @@ void setAmp(QuregImpl& q, i64 local, real re, real im) {
 
 void initDebug(QuregImpl& q, i64 globalOffset) {
     flush(q);
+#pragma omp parallel for if (q.numAmpsPerChunk >= kOmpMin)
     for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
         i64 g = globalOffset + i;
         q.re[i] = (real)((g * 2.0) / 10.0);
@@ -382,6 +393,7 @@ void initDebug(QuregImpl& q, i64 globalOffset) {
 
 void fillWhereBit(QuregImpl& q, int bit, int outcome, real val) {
     flush(q);
+#pragma omp parallel for if (q.numAmpsPerChunk >= kOmpMin)
     for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
         q.re[i] = (((i >> bit) & 1) == outcome) ? val : 0;
         q.im[i] = 0;
@@ -410,6 +422,7 @@ void copyState(QuregImpl& dst, QuregImpl& src) {
 double sumSq(QuregImpl& q, int bit, int bitVal) {
     flush(q);
     double s = 0;
+#pragma omp parallel for reduction(+ : s) if (q.numAmpsPerChunk >= kOmpMin)
     for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
         if (bit >= 0 && (int)((i >> bit) & 1) != bitVal) continue;
         s += (double)q.re[i] * q.re[i] + (double)q.im[i] * q.im[i];
@@ -421,6 +434,7 @@ void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]) {
     flush(bra);
     flush(ket);
     double r = 0, i = 0;
+#pragma omp parallel for reduction(+ : r, i) if (bra.numAmpsPerChunk >= kOmpMin)
     for (i64 k = 0; k < bra.numAmpsPerChunk; k++) {
         r += (double)bra.re[k] * ket.re[k] + (double)bra.im[k] * ket.im[k];
         i += (double)bra.re[k] * ket.im[k] - (double)bra.im[k] * ket.re[k];
@@ -447,6 +461,7 @@ double densDiagSum(QuregImpl& q, const u64* offs, int n, int skipBit, i64 chunkS
 void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
     flush(a);
     flush(b);
+#pragma omp parallel for if (a.numAmpsPerChunk >= kOmpMin)
     for (i64 i = 0; i < a.numAmpsPerChunk; i++) {
         a.re[i] = alpha * a.re[i] + beta * b.re[i];
         a.im[i] = alpha * a.im[i] + beta * b.im[i];
@@ -456,6 +471,7 @@ void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
 void densInitPure(QuregImpl& rho, const real* pr, const real* pi, int n, i64 chunkStart) {
     flush(rho);
     const i64 mask = ((i64)1 << n) - 1;
+#pragma omp parallel for if (rho.numAmpsPerChunk >= kOmpMin)
     for (i64 k = 0; k < rho.numAmpsPerChunk; k++) {
         i64 g = chunkStart + k, r = g & mask, c = g >> n;
         // psi_r * conj(psi_c)
