@@ -158,9 +158,15 @@ class _Binding:
             self._err.value = (int(code), msg.decode(), func.decode())
 
         self._handler = HANDLER(_handler)  # keep alive
+        self._null_handler = HANDLER()
         lib.setQuESTErrorHandler.argtypes = [HANDLER]
         lib.setQuESTErrorHandler.restype = None
         lib.setQuESTErrorHandler(self._handler)
+
+    def exit_on_error(self, enabled: bool = True):
+        """True: the reference's behaviour (print, then exit(code));
+        False (default): raise QuESTError."""
+        self.lib.setQuESTErrorHandler(self._null_handler if enabled else self._handler)
 
     # -- conversions ---------------------------------------------------------
     def to_complex(self, z) -> "C.Structure":

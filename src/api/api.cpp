@@ -326,7 +326,12 @@ void reportState(Qureg qureg) {
 
 void reportStateToScreen(Qureg qureg, QuESTEnv env, int reportRank) {
     QuregImpl& q = Q(qureg);
-    if (q.nSV > 5) return;
+    if (q.nSV > 5) {
+        // as the reference's host build (QuEST_cpu.c:1275); E_SYS_TOO_BIG_TO_PRINT is never raised there
+        if (q.chunkId == 0) printf("Error: reportStateToScreen will not print output for systems of more than 5 qubits.\n");
+        fflush(stdout);
+        return;
+    }
     std::vector<real> re((size_t)q.numAmpsPerChunk), im(re.size());
     router::readChunk(q, re.data(), im.data());
     for (int r = 0; r < q.numChunks; r++) {
