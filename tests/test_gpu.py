@@ -260,3 +260,28 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, ranks):
             assert str(got[k]) == v, k
         else:
             np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+
+
+def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
+    """The fork's 30-qubit benchmark program (examples/random_circuit_benchmark.c
+    flow: 490 gates, then P(q_i=1) for all 30 qubits and 10 amplitudes) on the
+    GPU; the outputs must equal, to the printed digits, those of the host
+    (CPU, OpenMP) build recorded in tests/data/fork_circuit_*_cpu.dat."""
+    import quest_amd as qa
+    from quest_amd.models import fork_circuit
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = qa.Register(genv, 30)
+    r.init_zero()
+    fork_circuit().apply(r)
+    probs = [r.prob(i, 1) for i in range(30)]
+    amps = [r.amp(i) for i in range(10)]
+    want_p = [float(l.split(":")[1]) for l in open(os.path.join(here, "data", "fork_circuit_probs_cpu.dat"))
+              if l.startswith("Probability")]
+    want_a = [complex(*map(float, l.split(":")[1].split(","))) for l in
+              open(os.path.join(here, "data", "fork_circuit_amps_cpu.dat"))]
+    assert len(want_p) == 30 and len(want_a) == 10
+    np.testing.assert_allclose(probs, want_p, atol=1.5e-6)
+    np.testing.assert_allclose(np.array(amps), np.array(want_a), atol=1.5e-6)
+    assert abs(r.total_prob() - 1) < 1e-10
+    r.close()
