@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Every benchmark configuration named in BASELINE.json, on one GPU:
+
+  tutorial    3-qubit tutorial circuit (plumbing; P(|111>), P(q2=1))
+  sweep       single-qubit-gate time vs #qubits (the headline metric, unfused:
+              one hadamard = one pass over the state), n = 20..34, targets
+              low / middle / high
+  random30    30-qubit fp64 depth-30 random layered circuit (fused)
+  fork30      the fork's exact 30-qubit benchmark program (490 gates,
+              30 calcProbOfOutcome, 10 getAmp; tutorial_example.c), wall time
+              vs its published 3783.93 s estimate
+  q34         34 qubits (256 GiB state, one MI355X): single gates + 2 layers
+  density17   17-qubit density matrix (also 2^34 amplitudes) + damping on
+              every qubit + gates
+
+    python tools/bench_suite.py [--only sweep,fork30] [--max-qubits 34] [--out f.json]
+"""
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+FORK_ESTIMATE_S = 3783.9266747315614
+
+
+def timed(fn, reps=5, sync=None):
+    ts = []
+    for _ in range(reps):
+        if sync:
+            sync()
+        t0 = time.perf_counter()
+        fn()
+        if sync:
+            sync()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts), min(ts)
+
+
+def run_tutorial(env, res):
+    import quest_amd as qa
+
+    q = qa.Register(env, 3)  # examples/tutorial_example.c
+    q.init_zero()
+    q.h(0)
+    q.cnot(0, 1)
+    q.ry(2, 0.1)
+    q.mcz([0, 1, 2])
+    u = [[0.5 + 0.5j, 0.5 - 0.5j], [0.5 - 0.5j, 0.5 + 0.5j]]
+    q.unitary(0, u)
+    q.compact(1, 0.5 + 0.5j, 0.5 - 0.5j)
+    q.rotate(2, 3.14 / 2, (1, 0, 0))
+    q.ccompact(0, 1, 0.5 + 0.5j, 0.5 - 0.5j)
+    q.mcunitary([0, 1], 2, u)
+    res["tutorial"] = {"prob_111": abs(q.amp(7)) ** 2, "prob_q2_1": q.prob(2, 1),
+                       "reference": {"prob_111": 0.498751, "prob_q2_1": 0.749178}}
+    q.close()
+
+
+def run_sweep(env, res, max_q):
+    import quest_amd as qa
+    from quest_amd.ops import capi
+
+    capi.setGateFusion(0)
+    out = []
+    for n in range(20, max_q + 1, 2):
+        r = qa.Register(env, n)
+        r.init_plus()
+        row = {"qubits": n, "bytes_per_gate": 2 * 16 * (1 << n)}
+        for label, t in (("t0", 0), ("mid", n // 2), ("top", n - 1)):
+            med, mn = timed(lambda: r.h(t), reps=7 if n < 32 else 3, sync=r.sync)
+            row[f"h_{label}_s"] = med
+        med, _ = timed(lambda: r.t(n // 2), reps=7 if n < 32 else 3, sync=r.sync)
+        row["t_mid_s"] = med
+        row["h_mid_TBps"] = row["bytes_per_gate"] / row["h_mid_s"] / 1e12
+        out.append(row)
+        print(f"sweep n={n}: H t=0 {row['h_t0_s']*1e3:.3f} ms, mid {row['h_mid_s']*1e3:.3f} ms "
+              f"({row['h_mid_TBps']:.2f} TB/s), top {row['h_top_s']*1e3:.3f} ms, T {row['t_mid_s']*1e3:.3f} ms",
+              flush=True)
+        r.close()
+    capi.setGateFusion(1)
+    res["sweep"] = out
+
+
+def run_random30(env, res):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    n, depth = 30, 30
+    c = random_layered(n, depth, seed=30)
+    r = qa.Register(env, n)
+    r.init_plus()
+    r.sync()
+    capi.resetQuESTStats()
+    t0 = time.perf_counter()
+    c.apply(r)
+    r.sync()
+    dt = time.perf_counter() - t0
+    st = capi.getQuESTStats()
+    res["random30"] = {"gates": len(c.gates), "seconds": dt, "s_per_gate": dt / len(c.gates),
+                       "passes": st["passes"], "norm_error": abs(r.total_prob() - 1)}
+    print(f"random30: {len(c.gates)} gates in {dt:.3f} s ({1e3 * dt / len(c.gates):.3f} ms/gate, "
+          f"{st['passes']} passes)", flush=True)
+    r.close()
+
+
+def run_fork30(env, res):
+    import quest_amd as qa
+    from quest_amd.models import fork_circuit
+
+    c = fork_circuit()
+    t0 = time.perf_counter()
+    r = qa.Register(env, 30)
+    c.apply(r)
+    probs = [r.prob(i, 1) for i in range(30)]
+    amps = [r.amp(i) for i in range(10)]
+    dt = time.perf_counter() - t0
+    res["fork30"] = {"seconds": dt, "estimate_s": FORK_ESTIMATE_S, "speedup": FORK_ESTIMATE_S / dt,
+                     "gates": len(c.gates), "prob_q0": probs[0], "amp0": [amps[0].real, amps[0].imag]}
+    print(f"fork30: {dt:.3f} s (fork estimate {FORK_ESTIMATE_S:.1f} s, x{FORK_ESTIMATE_S / dt:.0f})", flush=True)
+    r.close()
+
+
+def run_q34(env, res, n=34):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    r = qa.Register(env, n)
+    r.init_plus()
+    capi.setGateFusion(0)
+    single = {}
+    for label, t in (("t0", 0), ("mid", n // 2), ("top", n - 1)):
+        single[label], _ = timed(lambda: r.h(t), reps=3, sync=r.sync)
+    capi.setGateFusion(1)
+    c = random_layered(n, 2, seed=34)
+    r.sync()
+    t0 = time.perf_counter()
+    c.apply(r)
+    r.sync()
+    dt = time.perf_counter() - t0
+    res["q34"] = {"qubits": n, "state_GiB": 16 * (1 << n) / 2 ** 30, "h_single_s": single,
+                  "layered_gates": len(c.gates), "layered_s_per_gate": dt / len(c.gates),
+                  "norm_error": abs(r.total_prob() - 1)}
+    print(f"q{n}: H {single}, layered {1e3 * dt / len(c.gates):.2f} ms/gate", flush=True)
+    r.close()
+
+
+def run_density17(env, res, n=17):
+    import quest_amd as qa
+
+    d = qa.Register(env, n, density=True)
+    d.init_plus()
+    d.sync()
+    t0 = time.perf_counter()
+    for q in range(n):
+        d.damping(q, 0.1)
+    d.sync()
+    t_damp = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    for q in range(n):
+        d.h(q)
+    for q in range(0, n - 1, 2):
+        d.cnot(q, q + 1)
+    d.sync()
+    ng = n + len(range(0, n - 1, 2))
+    t_gate = (time.perf_counter() - t0) / ng
+    tr = d.total_prob()
+    pur = d.purity()
+    res["density17"] = {"qubits": n, "amps": 1 << (2 * n), "damping_s_per_channel": t_damp,
+                        "gate_s": t_gate, "trace": tr, "purity": pur}
+    print(f"density{n}: damping {1e3 * t_damp:.2f} ms/channel, gates {1e3 * t_gate:.2f} ms/gate, "
+          f"trace {tr:.12f}, purity {pur:.6f}", flush=True)
+    d.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="tutorial,sweep,random30,fork30,q34,density17")
+    ap.add_argument("--max-qubits", type=int, default=34)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import quest_amd as qa
+    from quest_amd.ops import capi
+
+    env = qa.Env()
+    res = {"backend": capi.getQuESTBackend(), "precision": capi.getQuEST_PREC()}
+    todo = args.only.split(",")
+    if "tutorial" in todo:
+        run_tutorial(env, res)
+    if "sweep" in todo:
+        run_sweep(env, res, args.max_qubits)
+    if "random30" in todo:
+        run_random30(env, res)
+    if "fork30" in todo:
+        run_fork30(env, res)
+    if "q34" in todo and args.max_qubits >= 34:
+        run_q34(env, res)
+    if "density17" in todo and args.max_qubits >= 34:
+        run_density17(env, res)
+    text = json.dumps(res, indent=1)
+    print(text)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(text)
+
+
+if __name__ == "__main__":
+    main()
