@@ -116,12 +116,19 @@ def run_fork30(env, res):
     c = fork_circuit()
     t0 = time.perf_counter()
     r = qa.Register(env, 30)
+    r.sync()
+    t1 = time.perf_counter()
     c.apply(r)
+    r.sync()
+    t2 = time.perf_counter()
     probs = [r.prob(i, 1) for i in range(30)]
+    t3 = time.perf_counter()
     amps = [r.amp(i) for i in range(10)]
-    dt = time.perf_counter() - t0
+    t4 = time.perf_counter()
+    dt = t4 - t0
     res["fork30"] = {"seconds": dt, "estimate_s": FORK_ESTIMATE_S, "speedup": FORK_ESTIMATE_S / dt,
-                     "gates": len(c.gates), "prob_q0": probs[0], "amp0": [amps[0].real, amps[0].imag]}
+                     "gates": len(c.gates), "create_s": t1 - t0, "gates_s": t2 - t1, "probs_s": t3 - t2,
+                     "amps_s": t4 - t3, "prob_q0": probs[0], "amp0": [amps[0].real, amps[0].imag]}
     print(f"fork30: {dt:.3f} s (fork estimate {FORK_ESTIMATE_S:.1f} s, x{FORK_ESTIMATE_S / dt:.0f})", flush=True)
     r.close()
 
