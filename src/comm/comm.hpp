@@ -31,6 +31,17 @@ bool active();  // true when size > 1
 // Exchange `bytes` with `peer`: send from `send`, receive into `recv`
 // (both backend comm buffers; must not overlap).
 void sendrecv(int peer, const void* send, void* recv, size_t bytes);
+// Simultaneous exchanges with several peers (each peer at most once; send
+// and recv buffers distinct).  Every rank lists its peers in increasing
+// order of (peer XOR rank), so that transports that pair ranks one at a time
+// proceed through perfect matchings and cannot deadlock.
+struct Xfer {
+    int peer;
+    const void* send;
+    void* recv;
+    size_t bytes;
+};
+void exchange(const Xfer* x, int n);
 // In-place sum of host doubles across ranks.
 void allreduceSum(double* vals, int n);
 // In-place logical AND of a host int across ranks.

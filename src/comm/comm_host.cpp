@@ -19,6 +19,9 @@ void finalize() {
 }
 bool active() { return g_size > 1; }
 void sendrecv(int peer, const void* send, void* recv, size_t bytes) { sock::sendrecv(peer, send, recv, bytes); }
+void exchange(const Xfer* x, int n) {
+    for (int i = 0; i < n; i++) sock::sendrecv(x[i].peer, x[i].send, x[i].recv, x[i].bytes);
+}
 void allreduceSum(double* vals, int n) { sock::allreduceSum(vals, n); }
 int allreduceAnd(int v) {
     double d = v ? 0.0 : 1.0;  // count failures

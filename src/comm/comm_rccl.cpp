@@ -185,6 +185,20 @@ void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
     QA_NCCL(R.groupEnd(), "ncclGroupEnd");
 }
 
+void exchange(const Xfer* x, int n) {
+    if (g_socket || g_size == 1) {
+        for (int i = 0; i < n; i++) sendrecv(x[i].peer, x[i].send, x[i].recv, x[i].bytes);
+        return;
+    }
+    // one group: RCCL drives every peer's xGMI link at once
+    QA_NCCL(R.groupStart(), "ncclGroupStart");
+    for (int i = 0; i < n; i++) {
+        QA_NCCL(R.send(x[i].send, x[i].bytes, ncclUint8, x[i].peer, g_comm, S()), "ncclSend");
+        QA_NCCL(R.recv(x[i].recv, x[i].bytes, ncclUint8, x[i].peer, g_comm, S()), "ncclRecv");
+    }
+    QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+}
+
 void allreduceSum(double* vals, int n) {
     if (g_size == 1) return;
     if (g_socket) {

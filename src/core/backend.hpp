@@ -66,11 +66,12 @@ void densInitPure(QuregImpl& rho, const real* psiRe, const real* psiIm, int n, i
 double densFidelity(QuregImpl& rho, const real* psiRe, const real* psiIm, int n, i64 chunkStart);
 
 // ---- distributed support -----------------------------------------------------
-// Gather / scatter the amplitudes whose local bit `bit` == bitVal, in
-// increasing index order, items [start, start+count) of that sub-sequence.
-void packBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, real* bufRe, real* bufIm);
-void unpackBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, const real* bufRe,
-               const real* bufIm);
+// Gather / scatter the amplitudes whose local bits pos[0..k) equal the
+// matching bits of setMask (k <= 8), in increasing index order: items
+// [start, start+count) of that sub-sequence.
+void packBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, real* bufRe, real* bufIm);
+void unpackBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, const real* bufRe,
+                const real* bufIm);
 // chunk amplitudes [local, local+n) -> comm buffer / comm buffer -> chunk
 void toBuffer(QuregImpl& q, i64 local, i64 n, real* bufRe, real* bufIm);
 void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* bufRe, const real* bufIm);

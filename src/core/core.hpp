@@ -73,6 +73,7 @@ struct QuregImpl {
     i64 useClock = 0;    // LRU bookkeeping for choosing swap victims
     i64 lastUse[64];
     std::vector<Op> pending;  // ops queued for fusion (backend-owned semantics)
+    std::vector<Op> lpending; // distributed registers: ops in LOGICAL qubits awaiting routing
     void* be = nullptr;       // backend-private state
     real* hostRe = nullptr;   // optional host mirror (Qureg.stateVec)
     real* hostIm = nullptr;

@@ -29,77 +29,201 @@ namespace router {
 
 namespace {
 
-// Reusable comm buffers for sliced exchanges: [re | im] for send and recv.
+// Reusable comm buffers for sliced exchanges: per peer [re | im], send and recv.
 struct XBuf {
-    real* send = nullptr;
-    real* recv = nullptr;
-    i64 amps = 0;  // capacity in amplitudes (per re/im half)
+    std::vector<real*> send, recv;
+    i64 amps = 0;  // capacity per buffer in amplitudes (per re/im half)
 } g_x;
 
-void ensureXBuf(i64 amps) {
-    if (g_x.amps >= amps) return;
-    if (g_x.send) be::freeComm(g_x.send);
-    if (g_x.recv) be::freeComm(g_x.recv);
-    g_x.send = (real*)be::allocComm(sizeof(real) * 2 * amps);
-    g_x.recv = (real*)be::allocComm(sizeof(real) * 2 * amps);
+void ensureXBuf(int peers, i64 amps) {
+    if ((int)g_x.send.size() >= peers && g_x.amps >= amps) return;
+    for (real* p : g_x.send) be::freeComm(p);
+    for (real* p : g_x.recv) be::freeComm(p);
+    g_x.send.assign(peers, nullptr);
+    g_x.recv.assign(peers, nullptr);
+    for (int i = 0; i < peers; i++) {
+        g_x.send[i] = (real*)be::allocComm(sizeof(real) * 2 * amps);
+        g_x.recv[i] = (real*)be::allocComm(sizeof(real) * 2 * amps);
+    }
     g_x.amps = amps;
 }
 
 inline int chunkBit(const QuregImpl& q, int phys) { return (q.chunkId >> (phys - q.L)) & 1; }
 
-void touch(QuregImpl& q, int phys) { q.lastUse[phys] = ++q.useClock; }
+inline bool distributed(const QuregImpl& q) { return q.L < q.nSV; }
 
-// Swap the qubit at global position g with the one at local position l.
-// Pairs of ranks differing in rank bit (g - L) exchange the half of their
-// chunk whose local bit l differs from their own rank bit, in slices.
-void swapGlobalLocal(QuregImpl& q, int g, int l) {
-    be::flush(q);
-    const int rbit = g - q.L;
-    const int partner = q.chunkId ^ (1 << rbit);
-    const int b = (q.chunkId >> rbit) & 1;
-    const i64 half = q.numAmpsPerChunk / 2;
-    i64 slice = rt().exchangeSliceBytes / (i64)(2 * sizeof(real));
-    if (slice < 1) slice = 1;
-    slice = std::min(slice, half);
-    ensureXBuf(slice);
-    for (i64 off = 0; off < half; off += slice) {
-        i64 n = std::min(slice, half - off);
-        be::packBit(q, l, 1 - b, off, n, g_x.send, g_x.send + n);
-        comm::sendrecv(partner, g_x.send, g_x.recv, sizeof(real) * 2 * (size_t)n);
-        be::unpackBit(q, l, 1 - b, off, n, g_x.recv, g_x.recv + n);
-        stats().bytesExchanged += (long long)(sizeof(real) * 2 * n);
-    }
-    int lg = q.p2l[g], ll = q.p2l[l];
-    q.l2p[lg] = l;
-    q.l2p[ll] = g;
-    q.p2l[g] = ll;
-    q.p2l[l] = lg;
-    std::swap(q.lastUse[g], q.lastUse[l]);
-    stats().swaps++;
+void enqueue(QuregImpl& q, const Op& op) {
+    be::enqueue(q, op);
+    stats().opsQueued++;
 }
 
-// Make the given logical qubits local, never evicting a protected one.
-void ensureLocal(QuregImpl& q, const int* lq, int n, const int* protect, int np) {
-    if (q.L == q.nSV) return;
-    for (int i = 0; i < n; i++) {
-        int p = q.l2p[lq[i]];
-        if (p < q.L) continue;
-        // least-recently-used local position not holding a protected qubit
-        int victim = -1;
-        for (int v = q.L - 1; v >= 0; v--) {
-            int logical = q.p2l[v];
-            bool prot = false;
-            for (int k = 0; k < n && !prot; k++) prot = (lq[k] == logical);
-            for (int k = 0; k < np && !prot; k++) prot = (protect[k] == logical);
-            if (prot) continue;
-            if (victim < 0 || q.lastUse[v] < q.lastUse[victim]) victim = v;
-        }
-        if (victim < 0) {
-            fprintf(stderr, "QuEST: no local qubit available for a distributed swap\n");
-            exit(EXIT_FAILURE);
-        }
-        swapGlobalLocal(q, p, victim);
+// Exchange the qubits at global positions gpos[m] with those at local
+// positions lpos[m] (m < k) in ONE all-to-all among the 2^k ranks that
+// differ in those rank bits.  Part j of a chunk (its k local bits = j) goes to
+// the peer whose k rank bits = j and comes back from it into the same place,
+// so every rank sends (1 - 2^-k) of its chunk, 2^-k of it to each of 2^k - 1
+// peers at once -- over as many xGMI links.  A one-qubit swap (k = 1) is the
+// reference's pairwise half-chunk exchange; swapping all rank qubits at once
+// uses every link (QuEST_cpu_distributed.c:41-512 exchanges whole chunks,
+// pairwise, once per gate).
+void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
+    if (k <= 0) return;
+    be::flush(q);
+    // order by rank bit so that peers come in increasing (peer ^ rank) order
+    int gpos[8], lpos[8], idx[8];
+    for (int m = 0; m < k; m++) idx[m] = m;
+    std::sort(idx, idx + k, [&](int a, int b) { return gposIn[a] < gposIn[b]; });
+    for (int m = 0; m < k; m++) {
+        gpos[m] = gposIn[idx[m]];
+        lpos[m] = lposIn[idx[m]];
     }
+    int myG = 0;
+    for (int m = 0; m < k; m++) myG |= chunkBit(q, gpos[m]) << m;
+    const int parts = 1 << k;
+    const i64 partSize = q.numAmpsPerChunk >> k;
+    i64 slice = (rt().exchangeSliceBytes >> (k - 1)) / (i64)(2 * sizeof(real));
+    slice = std::max<i64>(slice, ((i64)16 << 20) / (i64)(2 * sizeof(real)));
+    slice = std::min(slice, partSize);
+    ensureXBuf(parts - 1, slice);
+    std::vector<comm::Xfer> xs(parts - 1);
+    std::vector<u64> setMask(parts);
+    for (int j = 0; j < parts; j++) {
+        u64 msk = 0;
+        for (int m = 0; m < k; m++)
+            if ((j >> m) & 1) msk |= 1ull << lpos[m];
+        setMask[j] = msk;
+    }
+    for (i64 off = 0; off < partSize; off += slice) {
+        const i64 n = std::min(slice, partSize - off);
+        for (int d = 1; d < parts; d++) {
+            const int j = myG ^ d;
+            int peer = q.chunkId;
+            for (int m = 0; m < k; m++)
+                if ((d >> m) & 1) peer ^= 1 << (gpos[m] - q.L);
+            be::packBits(q, lpos, k, setMask[j], off, n, g_x.send[d - 1], g_x.send[d - 1] + n);
+            xs[d - 1] = {peer, g_x.send[d - 1], g_x.recv[d - 1], sizeof(real) * 2 * (size_t)n};
+        }
+        comm::exchange(xs.data(), parts - 1);
+        for (int d = 1; d < parts; d++) {
+            const int j = myG ^ d;
+            be::unpackBits(q, lpos, k, setMask[j], off, n, g_x.recv[d - 1], g_x.recv[d - 1] + n);
+        }
+        stats().bytesExchanged += (long long)(sizeof(real) * 2 * n) * (parts - 1);
+    }
+    for (int m = 0; m < k; m++) {
+        const int g = gpos[m], l = lpos[m];
+        const int lg = q.p2l[g], ll = q.p2l[l];
+        q.l2p[lg] = l;
+        q.l2p[ll] = g;
+        q.p2l[g] = ll;
+        q.p2l[l] = lg;
+    }
+    stats().swaps += k;
+}
+
+u64 logicalTargets(const Op& op) {
+    u64 m = 0;
+    for (int i = 0; i < op.nt; i++) m |= 1ull << op.t[i];
+    return m;
+}
+
+// Logical op -> physical op for the backend.  Controls (and the phase mask
+// of a diagonal op) on rank bits are decided per rank: either this rank's
+// whole chunk satisfies them (dropped from the mask) or none of it does (the
+// op is skipped here) -- no communication.
+void issue(QuregImpl& q, const Op& lop) {
+    Op op = lop;
+    op.ctrl = 0;
+    for (int i = 0; i < lop.nt; i++) op.t[i] = q.l2p[lop.t[i]];
+    for (u64 c = lop.ctrl; c; c &= c - 1) {
+        const int p = q.l2p[__builtin_ctzll(c)];
+        if (p >= q.L) {
+            if (!chunkBit(q, p)) return;
+        } else {
+            op.ctrl |= 1ull << p;
+        }
+    }
+    enqueue(q, op);
+}
+
+// Choose the qubits to bring onto local positions for the queued ops (the
+// first one must become runnable) and swap them in with one all-to-all:
+// every rank qubit the queue still targets comes in, in order of first use,
+// displacing the local qubits whose first use lies furthest ahead (Belady),
+// as long as that is later than the incoming qubit's.
+void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
+    const int INF = 1 << 30;
+    int first[64];
+    for (int i = 0; i < 64; i++) first[i] = INF;
+    for (int i = 0; i < (int)lq.size(); i++)
+        for (int t = 0; t < lq[i].nt; t++)
+            if (first[lq[i].t[t]] == INF) first[lq[i].t[t]] = i;
+    const u64 need0 = logicalTargets(lq[0]);
+    std::vector<int> in, out;
+    for (int lg = 0; lg < q.nSV; lg++)
+        if (q.l2p[lg] >= q.L && first[lg] < INF) in.push_back(lg);
+    std::sort(in.begin(), in.end(), [&](int a, int b) { return first[a] < first[b]; });
+    for (int lg = 0; lg < q.nSV; lg++)
+        if (q.l2p[lg] < q.L && !((need0 >> lg) & 1)) out.push_back(lg);
+    std::stable_sort(out.begin(), out.end(), [&](int a, int b) { return first[a] > first[b]; });
+    int gp[8], lp[8], k = 0;
+    for (size_t i = 0; i < in.size() && i < out.size() && k < 8; i++) {
+        const bool required = (need0 >> in[i]) & 1;
+        if (!required && first[out[i]] <= first[in[i]]) break;
+        gp[k] = q.l2p[in[i]];
+        lp[k] = q.l2p[out[i]];
+        k++;
+    }
+    if (k == 0) {
+        fprintf(stderr, "QuEST: no local qubit available for a distributed swap\n");
+        exit(EXIT_FAILURE);
+    }
+    multiSwap(q, gp, lp, k);
+}
+
+// Route the logical queue of a distributed register: issue, in commutation-
+// respecting order, every op whose targets are local; when blocked, swap in
+// the qubits the remaining ops need; repeat.
+void flushLogical(QuregImpl& q) {
+    std::vector<Op>& lq = q.lpending;
+    while (!lq.empty()) {
+        u64 local = 0;
+        for (int lg = 0; lg < q.nSV; lg++)
+            if (q.l2p[lg] < q.L) local |= 1ull << lg;
+        std::vector<Op> rest;
+        rest.reserve(lq.size());
+        u64 blockedTg = 0, blockedTouch = 0;
+        for (const Op& op : lq) {
+            const u64 tg = logicalTargets(op), touch = tg | op.ctrl;
+            if (!(tg & blockedTouch) && !(touch & blockedTg) && !(tg & ~local)) {
+                issue(q, op);
+            } else {
+                rest.push_back(op);
+                blockedTg |= tg;
+                blockedTouch |= touch;
+            }
+        }
+        lq.swap(rest);
+        if (!lq.empty()) planSwap(q, lq);
+    }
+}
+
+constexpr size_t kLogicalWindow = 1024;
+
+// Accept a logical op: single-rank registers go straight to the backend.
+void submit(QuregImpl& q, const Op& lop) {
+    if (!distributed(q)) {
+        issue(q, lop);
+        return;
+    }
+    q.lpending.push_back(lop);
+    if (q.lpending.size() >= kLogicalWindow) flushLogical(q);
+}
+
+// Everything routed and handed to the backend (queue flushed, async).
+void drain(QuregImpl& q) {
+    flushLogical(q);
+    be::flush(q);
 }
 
 void resetLayout(QuregImpl& q) {
@@ -107,11 +231,6 @@ void resetLayout(QuregImpl& q) {
         q.l2p[i] = q.p2l[i] = i;
         q.lastUse[i] = 0;
     }
-}
-
-void enqueue(QuregImpl& q, const Op& op) {
-    be::enqueue(q, op);
-    stats().opsQueued++;
 }
 
 i64 logicalToPhysicalIndex(const QuregImpl& q, i64 idx) {
@@ -140,14 +259,14 @@ void create(QuregImpl& q, int nSV, bool density) {
 }
 
 void destroy(QuregImpl& q) {
-    be::flush(q);
+    drain(q);
     be::freeState(q);
 }
 
-void flush(QuregImpl& q) { be::flush(q); }
+void flush(QuregImpl& q) { drain(q); }
 
 void sync(QuregImpl& q) {
-    be::flush(q);
+    drain(q);
     be::deviceSync();
 }
 
@@ -156,71 +275,50 @@ void sync(QuregImpl& q) {
 // ---------------------------------------------------------------------------
 
 void mat2(QuregImpl& q, int target, const int* ctrls, int nc, const cplx m[4]) {
-    ensureLocal(q, &target, 1, ctrls, nc);
     Op op;
     op.kind = OpKind::Mat2;
     op.nt = 1;
-    op.t[0] = q.l2p[target];
-    touch(q, op.t[0]);
-    for (int i = 0; i < nc; i++) {
-        int p = q.l2p[ctrls[i]];
-        if (p >= q.L) {
-            if (!chunkBit(q, p)) return;  // this rank's amplitudes all fail the control
-        } else {
-            op.ctrl |= 1ull << p;
-        }
-    }
+    op.t[0] = target;
+    for (int i = 0; i < nc; i++) op.ctrl |= 1ull << ctrls[i];
     for (int i = 0; i < 4; i++) op.m[i] = m[i];
-    enqueue(q, op);
+    submit(q, op);
 }
 
 void diag(QuregImpl& q, const int* qubits, int nq, cplx term) {
     Op op;
     op.kind = OpKind::Diag;
     op.nt = 0;
-    for (int i = 0; i < nq; i++) {
-        int p = q.l2p[qubits[i]];
-        if (p >= q.L) {
-            if (!chunkBit(q, p)) return;
-        } else {
-            op.ctrl |= 1ull << p;
-        }
-    }
+    for (int i = 0; i < nq; i++) op.ctrl |= 1ull << qubits[i];
     op.m[0] = term;
-    enqueue(q, op);
+    submit(q, op);
 }
 
 void mat4(QuregImpl& q, int q0, int q1, const cplx m[16]) {
-    int t[2] = {q0, q1};
-    ensureLocal(q, t, 2, nullptr, 0);
     Op op;
     op.kind = OpKind::Mat4;
     op.nt = 2;
-    op.t[0] = q.l2p[q0];
-    op.t[1] = q.l2p[q1];
-    touch(q, op.t[0]);
-    touch(q, op.t[1]);
+    op.t[0] = q0;
+    op.t[1] = q1;
     for (int i = 0; i < 16; i++) op.m[i] = m[i];
-    enqueue(q, op);
+    submit(q, op);
 }
 
 void densChan2(QuregImpl& q, int r1, int r2, int c1, int c2, real offFac, real keep, real mix) {
-    int t[4] = {r1, r2, c1, c2};
-    ensureLocal(q, t, 4, nullptr, 0);
     Op op;
     op.kind = OpKind::DensChan2;
     op.nt = 4;
-    for (int i = 0; i < 4; i++) {
-        op.t[i] = q.l2p[t[i]];
-        touch(q, op.t[i]);
-    }
+    op.t[0] = r1;
+    op.t[1] = r2;
+    op.t[2] = c1;
+    op.t[3] = c2;
     op.m[0] = {offFac, 0};
     op.m[1] = {keep, 0};
     op.m[2] = {mix, 0};
-    enqueue(q, op);
+    submit(q, op);
 }
 
 void collapse(QuregImpl& q, int qubit, int outcome, real renorm) {
+    flushLogical(q);
     int p = q.l2p[qubit];
     if (p >= q.L) {
         Op op;
@@ -245,6 +343,7 @@ void collapse(QuregImpl& q, int qubit, int outcome, real renorm) {
 void densCollapse(QuregImpl& q, int qubit, int outcome, real prob) {
     // keep elements whose row bit (qubit) and column bit (qubit + n) both equal
     // the outcome; scale them by 1/prob (reference divides by p, not sqrt(p))
+    flushLogical(q);
     real s = (real)1 / prob;
     int r = q.l2p[qubit], c = q.l2p[qubit + q.nRep];
     bool rGlobal = r >= q.L, cGlobal = c >= q.L;
@@ -294,7 +393,7 @@ void densCollapse(QuregImpl& q, int qubit, int outcome, real prob) {
 // ---------------------------------------------------------------------------
 
 void initClassical(QuregImpl& q, i64 index) {
-    be::flush(q);
+    drain(q);
     resetLayout(q);
     be::fill(q, 0, 0);
     i64 start = (i64)q.chunkId * q.numAmpsPerChunk;
@@ -302,19 +401,19 @@ void initClassical(QuregImpl& q, i64 index) {
 }
 
 void initUniform(QuregImpl& q, real val) {
-    be::flush(q);
+    drain(q);
     resetLayout(q);
     be::fill(q, val, 0);
 }
 
 void initDebug(QuregImpl& q) {
-    be::flush(q);
+    drain(q);
     resetLayout(q);
     be::initDebug(q, (i64)q.chunkId * q.numAmpsPerChunk);
 }
 
 void initSingleQubit(QuregImpl& q, int qubit, int outcome, real val) {
-    be::flush(q);
+    drain(q);
     resetLayout(q);
     if (qubit >= q.L) {
         be::fill(q, chunkBit(q, qubit) == outcome ? val : (real)0, 0);
@@ -325,7 +424,7 @@ void initSingleQubit(QuregImpl& q, int qubit, int outcome, real val) {
 
 void setAmps(QuregImpl& q, i64 start, const real* re, const real* im, i64 n) {
     if (n == q.numAmpsTotal && start == 0) {
-        be::flush(q);
+        drain(q);
         resetLayout(q);
     } else {
         canonicalise(q);
@@ -336,8 +435,8 @@ void setAmps(QuregImpl& q, i64 start, const real* re, const real* im, i64 n) {
 }
 
 void clone(QuregImpl& dst, QuregImpl& src) {
-    be::flush(src);
-    be::flush(dst);
+    drain(src);
+    drain(dst);
     be::copyState(dst, src);
     memcpy(dst.l2p, src.l2p, sizeof dst.l2p);
     memcpy(dst.p2l, src.p2l, sizeof dst.p2l);
@@ -348,7 +447,7 @@ void clone(QuregImpl& dst, QuregImpl& src) {
 // Gather the full canonical pure state (2^n amps) onto every rank.
 static void gatherPure(QuregImpl& psi, real** fullRe, real** fullIm) {
     canonicalise(psi);
-    be::flush(psi);
+    drain(psi);
     i64 total = psi.numAmpsTotal, chunk = psi.numAmpsPerChunk;
     *fullRe = (real*)be::allocComm(sizeof(real) * total);
     *fullIm = (real*)be::allocComm(sizeof(real) * total);
@@ -366,7 +465,7 @@ static void gatherPure(QuregImpl& psi, real** fullRe, real** fullIm) {
 void densInitPure(QuregImpl& rho, QuregImpl& psi) {
     real *fr, *fi;
     gatherPure(psi, &fr, &fi);
-    be::flush(rho);
+    drain(rho);
     resetLayout(rho);
     be::densInitPure(rho, fr, fi, rho.nRep, (i64)rho.chunkId * rho.numAmpsPerChunk);
     be::freeComm(fr);
@@ -374,29 +473,46 @@ void densInitPure(QuregImpl& rho, QuregImpl& psi) {
 }
 
 void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
+    drain(a);  // routing may move qubits: compare layouts afterwards
+    drain(b);
     if (memcmp(a.l2p, b.l2p, sizeof(int) * a.nSV) != 0) {
         canonicalise(a);
         canonicalise(b);
     }
-    be::flush(a);
-    be::flush(b);
     be::axpby(a, alpha, b, beta);
 }
 
 void canonicalise(QuregImpl& q) {
-    be::flush(q);
+    drain(q);
     if (q.permIdentity()) return;
-    // 1. put the right logical qubit on every global position
-    for (int g = q.L; g < q.nSV; g++) {
-        if (q.p2l[g] == g) continue;
-        int x = q.l2p[g];
-        if (x < q.L) {
-            swapGlobalLocal(q, g, x);
-        } else {
-            int v = q.L - 1;
-            swapGlobalLocal(q, x, v);          // logical g -> local v
-            swapGlobalLocal(q, g, q.l2p[g]);   // logical g -> position g
+    // 1. the right logical qubit on every global position, in all-to-all
+    //    rounds: first every global position whose qubit is local comes in;
+    //    qubits stuck on the wrong global position are first moved out to
+    //    local positions that hold no rank qubit
+    for (int round = 0; round < 4; round++) {
+        int gp[8], lp[8], k = 0;
+        for (int g = q.L; g < q.nSV; g++)
+            if (q.p2l[g] != g && q.l2p[g] < q.L) {
+                gp[k] = g;
+                lp[k] = q.l2p[g];
+                k++;
+            }
+        if (k == 0) {
+            for (int g = q.L; g < q.nSV; g++) {
+                if (q.p2l[g] == g) continue;
+                for (int v = 0; v < q.L; v++) {
+                    bool used = q.p2l[v] >= q.L;
+                    for (int m = 0; m < k && !used; m++) used = lp[m] == v;
+                    if (used) continue;
+                    gp[k] = g;
+                    lp[k] = v;
+                    k++;
+                    break;
+                }
+            }
         }
+        if (k == 0) break;
+        multiSwap(q, gp, lp, k);
     }
     // 2. permute local qubits with local SWAP ops
     static const cplx kSwap[16] = {{1, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 0}, {0, 0},
@@ -417,7 +533,7 @@ void canonicalise(QuregImpl& q) {
         q.p2l[x] = li;
         q.p2l[i] = i;
     }
-    be::flush(q);
+    drain(q);
 }
 
 // ---------------------------------------------------------------------------
@@ -425,7 +541,7 @@ void canonicalise(QuregImpl& q) {
 // ---------------------------------------------------------------------------
 
 cplx getAmp(QuregImpl& q, i64 flatIndex) {
-    be::flush(q);
+    drain(q);
     i64 p = logicalToPhysicalIndex(q, flatIndex);
     int owner = (int)(p >> q.L);
     real v[2] = {0, 0};
@@ -440,7 +556,7 @@ static double allSum(double x) {
 }
 
 double probZero(QuregImpl& q, int qubit) {
-    be::flush(q);
+    drain(q);
     stats().reductions++;
     int p = q.l2p[qubit];
     double part;
@@ -452,13 +568,13 @@ double probZero(QuregImpl& q, int qubit) {
 }
 
 double sumSqAll(QuregImpl& q) {
-    be::flush(q);
+    drain(q);
     stats().reductions++;
     return allSum(be::sumSq(q, -1, 0));
 }
 
 static double densDiag(QuregImpl& q, int skipBit) {
-    be::flush(q);
+    drain(q);
     stats().reductions++;
     u64 offs[64];
     for (int j = 0; j < q.nRep; j++) offs[j] = (1ull << q.l2p[j]) | (1ull << q.l2p[j + q.nRep]);
@@ -470,12 +586,12 @@ double densProbZero(QuregImpl& q, int qubit) { return densDiag(q, qubit); }
 double densTrace(QuregImpl& q) { return densDiag(q, -1); }
 
 cplx inner(QuregImpl& bra, QuregImpl& ket) {
+    drain(bra);  // routing may move qubits: compare layouts afterwards
+    drain(ket);
     if (memcmp(bra.l2p, ket.l2p, sizeof(int) * bra.nSV) != 0) {
         canonicalise(bra);
         canonicalise(ket);
     }
-    be::flush(bra);
-    be::flush(ket);
     stats().reductions++;
     double v[2];
     be::innerProduct(bra, ket, v);
@@ -514,7 +630,7 @@ void readRange(QuregImpl& q, i64 start, real* re, real* im, i64 n) {
 }
 
 void writeChunk(QuregImpl& q, const real* re, const real* im) {
-    be::flush(q);
+    drain(q);
     resetLayout(q);
     be::writeAmps(q, 0, re, im, q.numAmpsPerChunk);
 }

@@ -494,19 +494,39 @@ double densFidelity(QuregImpl& rho, const real* pr, const real* pi, int n, i64 c
     return s;
 }
 
-void packBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, real* br, real* bi) {
+namespace {
+// positions sorted ascending, for bit insertion
+int sortedPositions(const int* pos, int k, int* out) {
+    for (int i = 0; i < k; i++) out[i] = pos[i];
+    std::sort(out, out + k);
+    return k;
+}
+}  // namespace
+
+void packBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, real* br, real* bi) {
     flush(q);
+    int sp[8];
+    sortedPositions(pos, k, sp);
+#pragma omp parallel for if (count >= kOmpMin)
     for (i64 j = 0; j < count; j++) {
-        i64 i = insertZero(start + j, bit) | ((i64)bitVal << bit);
+        i64 i = start + j;
+        for (int m = 0; m < k; m++) i = insertZero(i, sp[m]);
+        i |= (i64)setMask;
         br[j] = q.re[i];
         bi[j] = q.im[i];
     }
 }
 
-void unpackBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, const real* br, const real* bi) {
+void unpackBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, const real* br,
+                const real* bi) {
     flush(q);
+    int sp[8];
+    sortedPositions(pos, k, sp);
+#pragma omp parallel for if (count >= kOmpMin)
     for (i64 j = 0; j < count; j++) {
-        i64 i = insertZero(start + j, bit) | ((i64)bitVal << bit);
+        i64 i = start + j;
+        for (int m = 0; m < k; m++) i = insertZero(i, sp[m]);
+        i |= (i64)setMask;
         q.re[i] = br[j];
         q.im[i] = bi[j];
     }

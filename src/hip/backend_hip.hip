@@ -304,14 +304,15 @@ double densFidelity(QuregImpl& rho, const real* pr, const real* pi, int n, i64 c
     return reduceDensFidelity(rho.re, rho.im, rho.numAmpsPerChunk, pr, pi, n, chunkStart);
 }
 
-void packBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, real* br, real* bi) {
+void packBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, real* br, real* bi) {
     flush(q);
-    launchPackBit(q.re, q.im, bit, bitVal, start, count, br, bi, false);
+    launchPackBits(q.re, q.im, pos, k, setMask, start, count, br, bi, false);
 }
 
-void unpackBit(QuregImpl& q, int bit, int bitVal, i64 start, i64 count, const real* br, const real* bi) {
+void unpackBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, const real* br,
+                const real* bi) {
     flush(q);
-    launchPackBit(q.re, q.im, bit, bitVal, start, count, const_cast<real*>(br), const_cast<real*>(bi), true);
+    launchPackBits(q.re, q.im, pos, k, setMask, start, count, const_cast<real*>(br), const_cast<real*>(bi), true);
 }
 
 void toBuffer(QuregImpl& q, i64 local, i64 n, real* br, real* bi) {

@@ -1,6 +1,8 @@
 // State preparation, distributed pack/unpack and elementwise kernels.
 // All grid-stride, 256 threads, 16-byte vector accesses where the layout
 // allows; launched on the backend stream.
+#include <algorithm>
+
 #include "qa_hip.h"
 
 namespace qa {
@@ -54,20 +56,30 @@ __global__ __launch_bounds__(kThreads) void fillBitKernel(T* __restrict__ re, T*
     }
 }
 
-// gather (UNPACK=false) / scatter (UNPACK=true) of the amplitudes whose bit
-// `bit` == bitVal; VN consecutive items per thread when the runs allow it
+// Bit positions inserted into a packed index (ascending) and the values
+// they take.
+struct PackBits {
+    int k;
+    int pos[8];
+    long long setMask;
+};
+
+// gather (UNPACK=false) / scatter (UNPACK=true) of the amplitudes whose bits
+// pos[] equal those of setMask; VN consecutive items per thread when the
+// lowest inserted bit is above the vector width
 template <typename T, bool UNPACK, bool VEC>
-__global__ __launch_bounds__(kThreads) void packKernel(T* __restrict__ re, T* __restrict__ im, int bit, int bitVal,
+__global__ __launch_bounds__(kThreads) void packKernel(T* __restrict__ re, T* __restrict__ im, PackBits pb,
                                                        long long start, long long count, T* __restrict__ br,
                                                        T* __restrict__ bi) {
     using V = typename Vec16<T>::type;
     constexpr int VN = VEC ? Vec16<T>::n : 1;
-    const long long set = (long long)bitVal << bit;
     const long long units = count / VN;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
         const long long j = u * VN;
-        const long long i = ins0(start + j, bit) | set;
+        long long i = start + j;
+        for (int m = 0; m < pb.k; m++) i = ins0(i, pb.pos[m]);
+        i |= pb.setMask;
         if constexpr (VEC) {
             if constexpr (UNPACK) {
                 *reinterpret_cast<V*>(re + i) = *reinterpret_cast<const V*>(br + j);
@@ -158,27 +170,32 @@ void launchFillWhereBit(real* re, real* im, i64 n, int bit, int outcome, real va
     QA_HIP_CHECK(hipGetLastError());
 }
 
-void launchPackBit(const real* re, const real* im, int bit, int bitVal, i64 start, i64 count, real* br, real* bi,
-                   bool unpack) {
+void launchPackBits(const real* re, const real* im, const int* pos, int k, u64 setMask, i64 start, i64 count,
+                    real* br, real* bi, bool unpack) {
     constexpr int VN = Vec16<real>::n;
-    const bool vec = ((1ll << bit) >= VN) && (start % VN == 0) && (count % VN == 0);
+    PackBits pb;
+    pb.k = k;
+    for (int m = 0; m < 8; m++) pb.pos[m] = m < k ? pos[m] : 0;
+    std::sort(pb.pos, pb.pos + k);
+    pb.setMask = (long long)setMask;
+    const bool vec = (k == 0 || (1ll << pb.pos[0]) >= VN) && (start % VN == 0) && (count % VN == 0);
     real* r = const_cast<real*>(re);
     real* m = const_cast<real*>(im);
     const int g = gridFor(vec ? count / VN : count);
     if (unpack) {
         if (vec)
-            hipLaunchKernelGGL((packKernel<real, true, true>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
-                               bitVal, start, count, br, bi);
+            hipLaunchKernelGGL((packKernel<real, true, true>), dim3(g), dim3(kThreads), 0, stream(), r, m, pb, start,
+                               count, br, bi);
         else
-            hipLaunchKernelGGL((packKernel<real, true, false>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
-                               bitVal, start, count, br, bi);
+            hipLaunchKernelGGL((packKernel<real, true, false>), dim3(g), dim3(kThreads), 0, stream(), r, m, pb, start,
+                               count, br, bi);
     } else {
         if (vec)
-            hipLaunchKernelGGL((packKernel<real, false, true>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
-                               bitVal, start, count, br, bi);
+            hipLaunchKernelGGL((packKernel<real, false, true>), dim3(g), dim3(kThreads), 0, stream(), r, m, pb,
+                               start, count, br, bi);
         else
-            hipLaunchKernelGGL((packKernel<real, false, false>), dim3(g), dim3(kThreads), 0, stream(), r, m, bit,
-                               bitVal, start, count, br, bi);
+            hipLaunchKernelGGL((packKernel<real, false, false>), dim3(g), dim3(kThreads), 0, stream(), r, m, pb,
+                               start, count, br, bi);
     }
     QA_HIP_CHECK(hipGetLastError());
 }

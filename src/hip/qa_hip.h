@@ -70,8 +70,8 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op);
 void launchFill(real* re, real* im, i64 n, real vr, real vi);
 void launchInitDebug(real* re, real* im, i64 n, i64 offset);
 void launchFillWhereBit(real* re, real* im, i64 n, int bit, int outcome, real val);
-void launchPackBit(const real* re, const real* im, int bit, int bitVal, i64 start, i64 count, real* br, real* bi,
-                   bool unpack);
+void launchPackBits(const real* re, const real* im, const int* pos, int k, u64 setMask, i64 start, i64 count,
+                    real* br, real* bi, bool unpack);
 void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n);
 void launchDensInitPure(real* re, real* im, i64 n, const real* pr, const real* pi, int nq, i64 chunkStart);
 
