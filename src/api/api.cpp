@@ -25,6 +25,7 @@
 #include "../comm/comm.hpp"
 #include "../core/backend.hpp"
 #include "../core/router.hpp"
+#include "../core/tiles.hpp"
 #include "common.hpp"
 #include "qasm.hpp"
 #include "validation.hpp"
@@ -892,7 +893,11 @@ void setFusionMaxQubits(int numQubits) {
 }
 
 int setQuESTTuning(const char* key, int value) {
-    for (QuregImpl* q : liveQuregs()) be::flush(*q);
+    for (QuregImpl* q : liveQuregs()) router::flush(*q);
+    if (key && !strcmp(key, "fuse_blocks")) {
+        fuseBlocks() = value != 0;
+        return 1;
+    }
     return be::setTuning(key, value) ? 1 : 0;
 }
 

@@ -1,6 +1,8 @@
 #include "tiles.hpp"
 
 #include <algorithm>
+#include <complex>
+#include <cstdlib>
 #include <cstring>
 
 namespace qa {
@@ -59,6 +61,204 @@ void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k,
 
 }  // namespace
 
+namespace {
+
+using zc = std::complex<double>;
+
+// A run of gates on at most two qubits, multiplied into one matrix on the
+// host: 4x4 in the basis (bit 0 <-> s[0], bit 1 <-> s[1]); a one-qubit block
+// uses the top-left 2x2 as a matrix on s[0].
+struct Block {
+    int ns = 0;
+    int s[2] = {-1, -1};
+    zc m[4][4];
+    int first = -1;      // index of its first op in the input
+    int count = 0;       // ops absorbed
+    bool allDiag = true;
+};
+
+// The op as a 4x4 matrix in the basis of block b (whose support contains the
+// op's qubits).
+void embed(const Op& op, const Block& b, zc e[4][4]) {
+    auto bitOf = [&](int q) { return q == b.s[0] ? 0 : 1; };
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) e[r][c] = r == c ? 1.0 : 0.0;
+    const int dim = b.ns == 2 ? 4 : 2;
+    if (op.kind == OpKind::Diag) {
+        unsigned mask = 0;
+        for (u64 c = op.ctrl; c; c &= c - 1) mask |= 1u << bitOf(__builtin_ctzll(c));
+        for (int i = 0; i < dim; i++)
+            if ((i & mask) == mask) e[i][i] = zc(op.m[0].re, op.m[0].im);
+        return;
+    }
+    if (op.kind == OpKind::Mat2) {
+        const int tb = bitOf(op.t[0]);
+        unsigned cmask = 0;
+        for (u64 c = op.ctrl; c; c &= c - 1) cmask |= 1u << bitOf(__builtin_ctzll(c));
+        for (int i = 0; i < dim; i++) {
+            if ((i & cmask) != cmask || ((i >> tb) & 1)) continue;
+            const int j = i | (1 << tb);
+            e[i][i] = zc(op.m[0].re, op.m[0].im);
+            e[i][j] = zc(op.m[1].re, op.m[1].im);
+            e[j][i] = zc(op.m[2].re, op.m[2].im);
+            e[j][j] = zc(op.m[3].re, op.m[3].im);
+        }
+        return;
+    }
+    // Mat4 on (t0, t1): op index g = bit(t0) + 2 bit(t1)
+    const int b0 = bitOf(op.t[0]), b1 = bitOf(op.t[1]);
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            const int gr = ((r >> b0) & 1) | (((r >> b1) & 1) << 1);
+            const int gc = ((c >> b0) & 1) | (((c >> b1) & 1) << 1);
+            e[r][c] = zc(op.m[4 * gr + gc].re, op.m[4 * gr + gc].im);
+        }
+}
+
+void leftMultiply(Block& b, const zc e[4][4]) {
+    zc out[4][4];
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) {
+            zc acc = 0;
+            for (int k = 0; k < 4; k++) acc += e[r][k] * b.m[k][c];
+            out[r][c] = acc;
+        }
+    for (int r = 0; r < 4; r++)
+        for (int c = 0; c < 4; c++) b.m[r][c] = out[r][c];
+}
+
+// qubits an op touches, if it can join a two-qubit block (else -1)
+int support(const Op& op, int q[2]) {
+    int n = 0;
+    auto add = [&](int x) {
+        for (int i = 0; i < n; i++)
+            if (q[i] == x) return true;
+        if (n == 2) return false;
+        q[n++] = x;
+        return true;
+    };
+    if (op.kind == OpKind::DensChan2) return -1;
+    if (op.kind == OpKind::Mat4 && op.ctrl) return -1;
+    for (int i = 0; i < op.nt; i++)
+        if (!add(op.t[i])) return -1;
+    for (u64 c = op.ctrl; c; c &= c - 1)
+        if (!add(__builtin_ctzll(c))) return -1;
+    return n;
+}
+
+}  // namespace
+
+bool& fuseBlocks() {
+    static bool on = [] {
+        const char* e = getenv("QUEST_FUSE_BLOCKS");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+void fuseGates(std::vector<Op>& ops) {
+    const int n = (int)ops.size();
+    if (n < 2) return;
+    std::vector<Block> blocks;
+    std::vector<int> opBlock(n, -1);  // block of each op (-1: kept as is)
+    int last[64];                      // block last touching each qubit; -2 barrier, -1 none
+    for (int i = 0; i < 64; i++) last[i] = -1;
+    for (int i = 0; i < n; i++) {
+        const Op& op = ops[i];
+        int q[2];
+        const int ns = support(op, q);
+        if (ns < 0) {  // barrier on every qubit it touches
+            for (int t = 0; t < op.nt; t++) last[op.t[t]] = -2;
+            for (u64 c = op.ctrl; c; c &= c - 1) last[__builtin_ctzll(c)] = -2;
+            continue;
+        }
+        if (ns == 0) continue;  // global phase on the whole chunk: leave in place
+        // joinable block: every qubit of the op last touched by the same block
+        // (or by nothing), and the union support stays within two qubits
+        int bid = -1;
+        bool ok = true;
+        for (int k = 0; k < ns && ok; k++) {
+            const int l = last[q[k]];
+            if (l == -2) ok = false;
+            else if (l >= 0) {
+                if (bid >= 0 && bid != l) ok = false;
+                bid = l;
+            }
+        }
+        if (ok && bid >= 0) {
+            Block& b = blocks[bid];
+            int extra = 0, ex = -1;
+            for (int k = 0; k < ns; k++)
+                if (q[k] != b.s[0] && q[k] != b.s[1]) extra++, ex = q[k];
+            if (b.ns + extra > 2) ok = false;
+            else if (extra == 1) {  // grow a one-qubit block: M -> I (x) M on the new qubit
+                b.s[1] = ex;
+                b.ns = 2;
+                zc g[4][4];
+                for (int r = 0; r < 4; r++)
+                    for (int c = 0; c < 4; c++) g[r][c] = ((r >> 1) == (c >> 1)) ? b.m[r & 1][c & 1] : zc(0);
+                for (int r = 0; r < 4; r++)
+                    for (int c = 0; c < 4; c++) b.m[r][c] = g[r][c];
+            }
+        } else if (ok) {
+            bid = -1;
+        }
+        if (!ok) bid = -1;
+        if (bid < 0) {
+            // blocked by another block: start a new one (the op's qubits'
+            // previous blocks are closed for it)
+            Block b;
+            b.ns = ns;
+            b.s[0] = q[0];
+            b.s[1] = ns == 2 ? q[1] : -1;
+            for (int r = 0; r < 4; r++)
+                for (int c = 0; c < 4; c++) b.m[r][c] = r == c ? 1.0 : 0.0;
+            b.first = i;
+            blocks.push_back(b);
+            bid = (int)blocks.size() - 1;
+        }
+        Block& b = blocks[bid];
+        zc e[4][4];
+        embed(op, b, e);
+        leftMultiply(b, e);
+        b.count++;
+        b.allDiag = b.allDiag && op.kind == OpKind::Diag;
+        opBlock[i] = bid;
+        for (int k = 0; k < ns; k++) last[q[k]] = bid;
+    }
+    // emit: a block at the position of its first op; blocks of one op, or of
+    // diagonal ops only, keep their original ops
+    std::vector<Op> out;
+    out.reserve(n);
+    for (int i = 0; i < n; i++) {
+        const int bid = opBlock[i];
+        if (bid < 0 || blocks[bid].count == 1 || blocks[bid].allDiag) {
+            out.push_back(ops[i]);
+            continue;
+        }
+        const Block& b = blocks[bid];
+        if (b.first != i) continue;
+        Op f;
+        f.ctrl = 0;
+        if (b.ns == 1) {
+            f.kind = OpKind::Mat2;
+            f.nt = 1;
+            f.t[0] = b.s[0];
+            for (int r = 0; r < 2; r++)
+                for (int c = 0; c < 2; c++) f.m[2 * r + c] = {(real)b.m[r][c].real(), (real)b.m[r][c].imag()};
+        } else {
+            f.kind = OpKind::Mat4;
+            f.nt = 2;
+            f.t[0] = b.s[0];
+            f.t[1] = b.s[1];
+            for (int r = 0; r < 4; r++)
+                for (int c = 0; c < 4; c++) f.m[4 * r + c] = {(real)b.m[r][c].real(), (real)b.m[r][c].imag()};
+        }
+        out.push_back(f);
+    }
+    ops.swap(out);
+}
+
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out) {
     out.passes.clear();
     out.ops.clear();
@@ -68,11 +268,15 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
     const u64 low = (c >= 64) ? ~0ull : ((1ull << c) - 1);
     // high targets allowed per pass besides the always-present low bits
     const int highSlots = k - c;
-    const int n = (int)ops.size();
+    int n = (int)ops.size();
 
     if (!fuse) {
         for (int i = 0; i < n; i++) emitPass(ops, i, i + 1, targetMask(ops[i]), L, k, c, out);
         return;
+    }
+    if (fuseBlocks()) {
+        fuseGates(ops);
+        n = (int)ops.size();
     }
 
     // List scheduling with commutation: a pass greedily collects every queued

@@ -91,6 +91,15 @@ void planDenseBlocks(TileProgram& prog, int k, int R);
 // TileProgram::phases).
 void planPhases(TileProgram& prog, int k, int R);
 
+// Multiply runs of gates acting on at most two qubits into one 2x2 / 4x4
+// matrix each (a run may interleave with gates on other qubits; ops keep
+// their relative order where they do not commute).  Diagonal-only runs and
+// single gates are left as they are.
+void fuseGates(std::vector<Op>& ops);
+// Gate-block fusion in planTiles (env QUEST_FUSE_BLOCKS=0 / setQuESTTuning
+// "fuse_blocks" turn it off).
+bool& fuseBlocks();
+
 // Split `ops` (physical local positions, L local qubits) into passes of at
 // most kmax tile qubits (kmax >= cmin + 4).  With fuse=true ops are reordered
 // where they commute to fill each pass (`ops` is left in execution order);

@@ -15,13 +15,14 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 VARIANTS = {
+    "fused-noblocks": dict(fusion=1, tile_mode=0, direct_kernels=1, fuse_blocks=0),
     "fused-dense": dict(fusion=1, tile_mode=2, direct_kernels=1),
     "fused-opbyop": dict(fusion=1, tile_mode=0, direct_kernels=1),
     "fused-regphase": dict(fusion=1, tile_mode=1, direct_kernels=1),
     "eager-direct": dict(fusion=0, tile_mode=2, direct_kernels=1),
     "eager-tile": dict(fusion=0, tile_mode=2, direct_kernels=0),
 }
-DEFAULTS = {"tile_mode": 0, "direct_kernels": 1, "tile_wg_per_cu": 2}
+DEFAULTS = {"tile_mode": 0, "direct_kernels": 1, "tile_wg_per_cu": 2, "fuse_blocks": 1}
 
 
 def main():
@@ -30,6 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--circuit", default="layered", choices=["layered", "fork"])
     args = ap.parse_args()
 
     import quest_amd as qa
@@ -40,7 +42,12 @@ def main():
     n = args.qubits
     reg = qa.Register(env, n)
     reg.init_plus()
-    circ = random_layered(n, args.layers, seed=5)
+    if args.circuit == "fork":
+        from quest_amd.models import fork_circuit
+
+        circ = fork_circuit() if n == 30 else __import__("quest_amd.models", fromlist=["x"]).fork_benchmark(n=n)
+    else:
+        circ = random_layered(n, args.layers, seed=5)
     names = args.variants.split(",")
     times = {v: [] for v in names}
     passes = {}
