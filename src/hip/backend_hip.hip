@@ -48,6 +48,7 @@ Tuning& tuning() {
         x.directKernels = env("QUEST_DIRECT_KERNELS", 1);
         x.tileMode = env("QUEST_TILE_MODE", 0);
         x.tileWgPerCU = env("QUEST_TILE_WG_PER_CU", 2);
+        x.tileQubits = env("QUEST_TILE_QUBITS", 0);
         return x;
     }();
     return t;
@@ -77,7 +78,8 @@ static_assert(kMaxQueued * (sizeof(TileOp) + sizeof(TilePhase) + sizeof(real) * 
 
 int tileQubits(int L) {
     const int cmin = sizeof(real) == 8 ? 4 : 5;
-    int kmax = rt().fuseMaxQubits > 0 ? rt().fuseMaxQubits : (sizeof(real) == 8 ? 11 : 12);
+    int kmax = rt().fuseMaxQubits > 0 ? rt().fuseMaxQubits
+                                      : (tuning().tileQubits > 0 ? tuning().tileQubits : kTileQubits);
     kmax = std::min(kmax, 13);
     // keep at least ~128 tiles in flight for small chunks
     int k = std::min(kmax, std::max(cmin + 4, L - 7));
@@ -346,6 +348,7 @@ bool setTuning(const char* key, int value) {
     std::string k(key);
     if (k == "direct_kernels") hipk::tuning().directKernels = value;
     else if (k == "tile_mode") hipk::tuning().tileMode = value;
+    else if (k == "tile_qubits") hipk::tuning().tileQubits = value;
     else if (k == "tile_wg_per_cu") hipk::tuning().tileWgPerCU = value;
     else return false;
     return true;

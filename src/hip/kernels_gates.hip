@@ -458,7 +458,7 @@ __device__ __forceinline__ typename Vec16<T>::type ldsGetVec(const T* s, unsigne
 // vectors per array for the HBM <-> LDS moves.
 // MODE 0: ops one by one on LDS; 1: register phases; 2: dense blocks
 template <typename T, int K, int MODE>
-__global__ __launch_bounds__(256, MODE == 1 ? 2 : 4) void tilePassKernelK(T* __restrict__ re, T* __restrict__ im, TileArgs a,
+__global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void tilePassKernelK(T* __restrict__ re, T* __restrict__ im, TileArgs a,
                                                        const TileOp* __restrict__ ops,
                                                        const TilePhase* __restrict__ phases,
                                                        const real* __restrict__ mats) {
@@ -599,6 +599,11 @@ void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps, c
         else
             hipLaunchKernelGGL((tilePassKernelK<real, kTileQubits, 0>), dim3((int)g2), dim3(256), lds, stream(), re,
                                im, a, dOps, dPhases, dMats);
+    } else if (a.k == kTileQubits + 1 && a.c >= vecBits && a.nPhases == 0) {
+        // double tile (64 KiB of LDS): op by op, 2 resident workgroups per CU
+        const long long g2 = a.numTiles < (long long)numCUs() * 2 ? a.numTiles : (long long)numCUs() * 2;
+        hipLaunchKernelGGL((tilePassKernelK<real, kTileQubits + 1, 0>), dim3((int)g2), dim3(256), lds, stream(), re,
+                           im, a, dOps, dPhases, dMats);
     } else if (a.c >= vecBits) {
         hipLaunchKernelGGL((tilePassKernel<real, true>), dim3(grid), dim3(256), lds, stream(), re, im, a, dOps);
     } else {

@@ -28,6 +28,7 @@ struct Tuning {
     int directKernels = 1;  // LDS-free kernels for single-op passes
     int tileMode = 0;       // fused tiles: 0 op by op (default), 1 register phases, 2 dense blocks
     int tileWgPerCU = 2;    // grid of the register-phase tile kernel, per CU
+    int tileQubits = 0;     // tile bits of fused passes (0: kTileQubits; kTileQubits + 1 = 64 KiB tiles)
 };
 Tuning& tuning();
 
