@@ -74,6 +74,7 @@ struct QuregImpl {
     i64 lastUse[64];
     std::vector<Op> pending;  // ops queued for fusion (backend-owned semantics)
     std::vector<Op> lpending; // distributed registers: ops in LOGICAL qubits awaiting routing
+    bool jointAlloc = false;  // HIP: re and im share one allocation (freed through re)
     void* be = nullptr;       // backend-private state
     real* hostRe = nullptr;   // optional host mirror (Qureg.stateVec)
     real* hostIm = nullptr;

@@ -49,6 +49,8 @@ Tuning& tuning() {
         x.tileMode = env("QUEST_TILE_MODE", 0);
         x.tileWgPerCU = env("QUEST_TILE_WG_PER_CU", 2);
         x.tileQubits = env("QUEST_TILE_QUBITS", 0);
+        x.directLayout = env("QUEST_DIRECT_LAYOUT", 1);
+        x.directLowToTile = env("QUEST_DIRECT_LOW_TO_TILE", 1);
         return x;
     }();
     return t;
@@ -187,19 +189,39 @@ std::string describe() {
 const char* shortName() { return "HIP"; }
 bool stateOnHost() { return false; }
 
+// The re and im arrays of a register.  QUEST_ALLOC_MODE=1 places both in
+// one allocation, im starting QUEST_IM_OFFSET bytes after the end of re
+// (HBM channel / TLB placement experiments); the default is two allocations.
 void allocState(QuregImpl& q) {
     const size_t bytes = sizeof(real) * (size_t)q.numAmpsPerChunk;
+    const char* mode = getenv("QUEST_ALLOC_MODE");
+    if (mode && atoi(mode) == 1) {
+        const char* o = getenv("QUEST_IM_OFFSET");
+        size_t off = o ? (size_t)atoll(o) : 0;
+        off = (off + 255) & ~(size_t)255;
+        char* base = nullptr;
+        if (hipMalloc(&base, 2 * bytes + off) != hipSuccess) {
+            fprintf(stderr, "QuEST: out of device memory allocating 2 x %.2f GiB for a %d-qubit register\n",
+                    (double)bytes / (1 << 30), q.nSV);
+            exit(EXIT_FAILURE);
+        }
+        q.re = reinterpret_cast<real*>(base);
+        q.im = reinterpret_cast<real*>(base + bytes + off);
+        q.jointAlloc = true;
+        return;
+    }
     if (hipMalloc(&q.re, bytes) != hipSuccess || hipMalloc(&q.im, bytes) != hipSuccess) {
         fprintf(stderr, "QuEST: out of device memory allocating 2 x %.2f GiB for a %d-qubit register\n",
                 (double)bytes / (1 << 30), q.nSV);
         exit(EXIT_FAILURE);
     }
+    q.jointAlloc = false;
 }
 
 void freeState(QuregImpl& q) {
     deviceSync();
     (void)hipFree(q.re);
-    (void)hipFree(q.im);
+    if (!q.jointAlloc) (void)hipFree(q.im);
     q.re = q.im = nullptr;
 }
 
@@ -349,6 +371,8 @@ bool setTuning(const char* key, int value) {
     if (k == "direct_kernels") hipk::tuning().directKernels = value;
     else if (k == "tile_mode") hipk::tuning().tileMode = value;
     else if (k == "tile_qubits") hipk::tuning().tileQubits = value;
+    else if (k == "direct_layout") hipk::tuning().directLayout = value;
+    else if (k == "direct_low_to_tile") hipk::tuning().directLowToTile = value;
     else if (k == "tile_wg_per_cu") hipk::tuning().tileWgPerCU = value;
     else return false;
     return true;

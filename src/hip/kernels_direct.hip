@@ -48,21 +48,36 @@ __device__ __forceinline__ void mat2apply(const Cm2<T>& m, T& r0, T& i0, T& r1, 
     i1 = m.r[2] * b + m.i[2] * a + m.r[3] * d + m.i[3] * c;
 }
 
+// This thread's groups of UNR units: u0 + k * step, k < UNR.  BLK = false:
+// grid-stride (consecutive groups of one thread lie a whole grid apart);
+// BLK = true: each workgroup owns a contiguous run of 256 * UNR units, so
+// the UNR loads of a wave are 4 KiB apart instead of a grid's worth.
+template <bool BLK, int UNR, typename F>
+__device__ __forceinline__ void forUnits(long long units, F&& f) {
+    if constexpr (BLK) {
+        const long long per = (long long)blockDim.x * UNR;
+        for (long long c = blockIdx.x; c * per < units; c += gridDim.x) f(c * per + threadIdx.x, (long long)blockDim.x);
+    } else {
+        const long long stride = (long long)gridDim.x * blockDim.x;
+        for (long long u0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; u0 < units; u0 += stride * UNR)
+            f(u0, stride);
+    }
+}
+
 // target >= log2(VN): a vector at `up` (target bit 0) pairs with the vector
 // at up + 2^t.
-template <typename T>
+template <typename T, bool BLK>
 __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                         InsertBits ib, long long tbit, Cm2<T> m) {
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::n;
     constexpr int UNR = 2;
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long u0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; u0 < units; u0 += stride * UNR) {
+    forUnits<BLK, UNR>(units, [&](long long u0, long long step) {
         long long up[UNR];
         V ar[UNR], ai[UNR], br[UNR], bi[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
-            const long long u = u0 + k * stride;
+            const long long u = u0 + k * step;
             up[k] = u < units ? insertAll(u * VN, ib) : -1;
             if (up[k] >= 0) {
                 ar[k] = *reinterpret_cast<const V*>(re + up[k]);
@@ -88,23 +103,22 @@ __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* _
             *reinterpret_cast<V*>(re + up[k] + tbit) = br[k];
             *reinterpret_cast<V*>(im + up[k] + tbit) = bi[k];
         }
-    }
+    });
 }
 
 // target inside one vector (bit 0 for fp64, bits 0-1 for fp32)
-template <typename T>
+template <typename T, bool BLK>
 __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                      InsertBits ib, int t, Cm2<T> m) {
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::n;
     constexpr int UNR = 4;
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long u0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; u0 < units; u0 += stride * UNR) {
+    forUnits<BLK, UNR>(units, [&](long long u0, long long step) {
         long long at[UNR];
         V vr[UNR], vi[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
-            const long long u = u0 + k * stride;
+            const long long u = u0 + k * step;
             at[k] = u < units ? insertAll(u * VN, ib) : -1;
             if (at[k] >= 0) {
                 vr[k] = *reinterpret_cast<const V*>(re + at[k]);
@@ -126,23 +140,22 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
             *reinterpret_cast<V*>(re + at[k]) = vr[k];
             *reinterpret_cast<V*>(im + at[k]) = vi[k];
         }
-    }
+    });
 }
 
 // multiply the amplitudes whose mask bits are all 1
-template <typename T>
+template <typename T, bool BLK>
 __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                         InsertBits ib, T tr, T ti) {
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::n;
     constexpr int UNR = 4;
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long u0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; u0 < units; u0 += stride * UNR) {
+    forUnits<BLK, UNR>(units, [&](long long u0, long long step) {
         long long at[UNR];
         V vr[UNR], vi[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
-            const long long u = u0 + k * stride;
+            const long long u = u0 + k * step;
             at[k] = u < units ? insertAll(u * VN, ib) : -1;
             if (at[k] >= 0) {
                 vr[k] = *reinterpret_cast<const V*>(re + at[k]);
@@ -164,7 +177,7 @@ __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* _
             *reinterpret_cast<V*>(re + at[k]) = vr[k];
             *reinterpret_cast<V*>(im + at[k]) = vi[k];
         }
-    }
+    });
 }
 
 int directGrid(long long units) {
@@ -183,6 +196,14 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
     const long long N = 1ll << L;
     if (N < (long long)VN * 2048) return false;  // small states: one tile pass is as good
     if (op.kind != OpKind::Mat2 && op.kind != OpKind::Diag) return false;
+    const bool blk = tuning().directLayout == 1;
+    // Targets / masks inside a 128-byte line: the LDS tile pass streams
+    // faster than the in-register pair kernels (measured 6.7 vs 7.3-8.9 ms
+    // per H on 30 qubits, tools/layout_probe.py), so leave those to it.
+    if (tuning().directLowToTile) {
+        if (op.kind == OpKind::Mat2 && op.t[0] < LINE) return false;
+        if ((op.ctrl & ((1ull << LINE) - 1)) != 0) return false;
+    }
 
     InsertBits ib;
     ib.n = 0;
@@ -204,8 +225,12 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
         if (ni > 8) return false;
         for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
         const long long units = (N >> ni) / VN;
-        hipLaunchKernelGGL(diagDirectKernel<real>, dim3(directGrid(units)), dim3(256), 0, stream(), re, im, units, ib,
-                           op.m[0].re, op.m[0].im);
+        if (blk)
+            hipLaunchKernelGGL((diagDirectKernel<real, true>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
+                               units, ib, op.m[0].re, op.m[0].im);
+        else
+            hipLaunchKernelGGL((diagDirectKernel<real, false>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
+                               units, ib, op.m[0].re, op.m[0].im);
         QA_HIP_CHECK(hipGetLastError());
         return true;
     }
@@ -231,14 +256,22 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
         if (!placed) all[na++] = t;
         for (int i = 0; i < na; i++) ib.pos[ib.n++] = all[i];
         const long long units = (N >> na) / VN;
-        hipLaunchKernelGGL(mat2DirectKernel<real>, dim3(directGrid(units)), dim3(256), 0, stream(), re, im, units, ib,
-                           1ll << t, m);
+        if (blk)
+            hipLaunchKernelGGL((mat2DirectKernel<real, true>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
+                               units, ib, 1ll << t, m);
+        else
+            hipLaunchKernelGGL((mat2DirectKernel<real, false>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
+                               units, ib, 1ll << t, m);
     } else {
         if (ni > 8) return false;
         for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
         const long long units = (N >> ni) / VN;
-        hipLaunchKernelGGL(mat2LowKernel<real>, dim3(directGrid(units)), dim3(256), 0, stream(), re, im, units, ib, t,
-                           m);
+        if (blk)
+            hipLaunchKernelGGL((mat2LowKernel<real, true>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
+                               units, ib, t, m);
+        else
+            hipLaunchKernelGGL((mat2LowKernel<real, false>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
+                               units, ib, t, m);
     }
     QA_HIP_CHECK(hipGetLastError());
     return true;

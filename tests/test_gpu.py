@@ -285,3 +285,54 @@ def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
     np.testing.assert_allclose(np.array(amps), np.array(want_a), atol=1.5e-6)
     assert abs(r.total_prob() - 1) < 1e-10
     r.close()
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("low_to_tile", [0, 1])
+def test_direct_kernel_variants(genv, layout, low_to_tile):
+    """Unfused gates through every direct-kernel variant (unit order, low
+    targets in-register vs via the tile pass), 16 qubits, vs the oracle."""
+    import quest_amd as qa
+    from helpers import apply_random_ops, assert_close, oracle_for
+
+    qa.capi.setGateFusion(0)
+    qa.capi.setQuESTTuning("direct_layout", layout)
+    qa.capi.setQuESTTuning("direct_low_to_tile", low_to_tile)
+    try:
+        rng = np.random.default_rng(10 * layout + low_to_tile)
+        reg = qa.Register(genv, 16)
+        o = oracle_for(reg, rng)
+        apply_random_ops(reg, o, rng, 120)
+        for t in range(16):  # every target, incl. the in-vector ones
+            apply_random_ops(reg, o, rng, 0)
+            reg.h(t)
+            o.apply(np.array([[1, 1], [1, -1]]) / np.sqrt(2), t)
+            reg.t(t)
+            o.apply(np.diag([1, np.exp(1j * np.pi / 4)]), t)
+        assert_close(reg, o)
+        reg.close()
+    finally:
+        qa.capi.setGateFusion(1)
+        qa.capi.setQuESTTuning("direct_layout", 1)
+        qa.capi.setQuESTTuning("direct_low_to_tile", 1)
+
+
+def test_tile_qubits_12_matches_oracle(genv):
+    """The optional 64 KiB tile (tile_qubits = 12) on a long fused circuit."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.utils import oracle as O
+
+    qa.capi.setQuESTTuning("tile_qubits", 12)
+    try:
+        n = 20
+        c = random_layered(n, 8, seed=12)
+        reg = qa.Register(genv, n)
+        reg.init_plus()
+        c.apply(reg)
+        o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
+        c.apply_oracle(o)
+        assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
+        reg.close()
+    finally:
+        qa.capi.setQuESTTuning("tile_qubits", 0)
