@@ -336,3 +336,17 @@ def test_tile_qubits_12_matches_oracle(genv):
         reg.close()
     finally:
         qa.capi.setQuESTTuning("tile_qubits", 0)
+
+
+def test_reference_golden_suite_fp32_on_gpu():
+    """The fp32 HIP library on the golden data (subprocess: one precision per
+    process)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-m", "quest_amd.utils.golden", "--tol", "2e-4"], cwd=root,
+                         env=dict(os.environ, QUEST_BACKEND="hip", QUEST_PREC="1"), capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "773 passed, 0 failed" in out.stdout

@@ -45,6 +45,21 @@ def test_golden_suite_distributed(ranks):
     assert int(res[0].stdout.strip().split()[-4]) >= 770
 
 
+def test_golden_suite_fp32_build():
+    """The single-precision library (QuEST_PREC=1) on the same golden data
+    (relative tolerance 2e-4: fp32 cos/sin of the data's ~300 rad angles)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-m", "quest_amd.utils.golden", "--tol", "2e-4"], cwd=root,
+                         env=dict(os.environ, QUEST_BACKEND=os.environ.get("QUEST_BACKEND", "cpu"), QUEST_PREC="1"),
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "773 passed, 0 failed" in out.stdout
+
+
 # --- essential/state_vector ----------------------------------------------------------------
 
 def test_create_qureg_fields(env):
