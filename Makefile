@@ -18,7 +18,7 @@ BUILD     := build
 LIBDIR    := quest_amd/lib
 JOBS      ?= 8
 
-COMMON_SRC := src/api/api.cpp src/api/validation.cpp src/api/qasm.cpp src/api/common.cpp \
+COMMON_SRC := src/api/api.cpp src/api/validation.cpp src/api/qasm.cpp src/api/common.cpp src/api/checkpoint.cpp \
               src/api/mt19937.cpp src/core/router.cpp src/core/tiles.cpp src/comm/bootstrap.cpp
 CPU_SRC    := $(COMMON_SRC) src/comm/comm_socket.cpp src/comm/comm_host.cpp src/cpu/backend_cpu.cpp
 HIP_HOST   := $(COMMON_SRC) src/comm/comm_socket.cpp src/comm/comm_rccl.cpp

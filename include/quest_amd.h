@@ -55,6 +55,13 @@ void copyChunkFromBuffers(Qureg qureg, const qreal* re, const qreal* im);
  * every rank; the counterpart of setAmps. */
 void getAmps(Qureg qureg, long long int startInd, qreal* reals, qreal* imags, long long int numAmps);
 
+/* Binary checkpoint: every rank streams its (canonical) chunk to
+ * "<path>.<rank>" behind a 64-byte header.  Collective; returns 1 on success
+ * everywhere.  A checkpoint written by R ranks restores on any number of ranks
+ * (same qubits, register type and precision, else E_CHECKPOINT_MISMATCH). */
+int saveQuregCheckpoint(Qureg qureg, const char* path);
+int loadQuregCheckpoint(Qureg qureg, const char* path);
+
 /* Restore the canonical qubit layout after distributed qubit remapping. */
 void canonicaliseQureg(Qureg qureg);
 /* physical bit position of each logical qubit of the state-vector */

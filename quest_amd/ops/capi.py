@@ -144,6 +144,7 @@ class _Binding:
             "copyChunkFromBuffers": (v, [Q, C.c_void_p, C.c_void_p]), "canonicaliseQureg": (v, [Q]),
             "getQubitLayout": (v, [Q, ip]), "getAmps": (v, [Q, ll, rp, rp, ll]), "getQuESTStats": (v, [P(QuESTStats)]), "resetQuESTStats": (v, []),
             "getQuESTBackend": (C.c_char_p, []), "getQuESTSeeds": (v, [P(C.c_ulong), ip]),
+            "saveQuregCheckpoint": (i, [Q, C.c_char_p]), "loadQuregCheckpoint": (i, [Q, C.c_char_p]),
         }
         for name, (res, args) in self.protos.items():
             f = getattr(lib, name)
@@ -417,6 +418,14 @@ def setQuESTTuning(key: str, value: int) -> bool:
 
 def getQuESTBackend() -> str:
     return _call("getQuESTBackend").decode()
+
+
+def saveQuregCheckpoint(q, path) -> bool:
+    return bool(_call("saveQuregCheckpoint", q, str(path).encode()))
+
+
+def loadQuregCheckpoint(q, path) -> bool:
+    return bool(_call("loadQuregCheckpoint", q, str(path).encode()))
 
 
 def getQubitLayout(q) -> list:

@@ -106,6 +106,14 @@ class Register:
         else:
             capi.setAmps(self.q, start, a.real, a.imag, len(a))
 
+    def save(self, path):
+        """Binary checkpoint (every rank writes "<path>.<rank>")."""
+        return capi.saveQuregCheckpoint(self.q, path)
+
+    def load(self, path):
+        """Restore from a checkpoint written by save() on any number of ranks."""
+        return capi.loadQuregCheckpoint(self.q, path)
+
     def clone_from(self, other: "Register"):
         capi.cloneQureg(self.q, other.q)
 

@@ -44,6 +44,7 @@ static const char* kMessages[E_NUM_ERROR_CODES] = {
     "Too few qubits to distribute the register over this many ranks.",
     "Out of device memory while allocating the register.",
     "Device runtime error.",
+    "Checkpoint does not match the register (number of qubits, register type or precision).",
 };
 
 static QuESTErrorHandler g_handler = nullptr;

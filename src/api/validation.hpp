@@ -44,6 +44,7 @@ enum ErrorCode {
     E_TOO_MANY_QUBITS_FOR_RANKS,
     E_OUT_OF_MEMORY,
     E_DEVICE_ERROR,
+    E_CHECKPOINT_MISMATCH,
     E_NUM_ERROR_CODES
 };
 

@@ -629,6 +629,11 @@ void readRange(QuregImpl& q, i64 start, real* re, real* im, i64 n) {
     }
 }
 
+void prepareOverwrite(QuregImpl& q) {
+    drain(q);
+    resetLayout(q);
+}
+
 void writeChunk(QuregImpl& q, const real* re, const real* im) {
     drain(q);
     resetLayout(q);

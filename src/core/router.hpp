@@ -4,11 +4,12 @@
 // Replaces the reference's per-gate local/remote branching
 // (QuEST/src/CPU/QuEST_cpu_distributed.c:816-1214) with one mechanism:
 //  * each register keeps a logical->physical qubit map;
-//  * a non-diagonal op whose target sits on a global (rank) bit first swaps
-//    that qubit with a local one: each rank exchanges HALF its chunk with one
-//    partner over RCCL (the reference exchanges the full chunk, per gate);
-//    the map is updated instead of swapping back, so later gates on the same
-//    qubit stay local;
+//  * on a distributed register ops wait in a logical queue; routing issues,
+//    in commutation-respecting order, every op whose targets are local, and
+//    when blocked swaps in the rank qubits the queue needs, all at once, with
+//    ONE all-to-all among the 2^k ranks concerned (every peer's xGMI link at
+//    once; the reference exchanges a whole chunk pairwise, per gate); the map
+//    is updated instead of swapping back, so later gates stay local;
 //  * controls and diagonal bits on global qubits become per-rank predicates
 //    (no communication, and a rank whose control bit is 0 does nothing);
 //  * reductions are chunk partials + one allreduce.
@@ -58,6 +59,9 @@ double densFidelity(QuregImpl& rho, QuregImpl& psi);
 // read this rank's chunk in canonical order (host arrays of numAmpsPerChunk)
 void readChunk(QuregImpl& q, real* re, real* im);
 void writeChunk(QuregImpl& q, const real* re, const real* im);
+// route and flush everything queued, then reset the layout to canonical
+// without moving data: the caller overwrites the whole chunk next
+void prepareOverwrite(QuregImpl& q);
 // collective read of global amplitudes [start, start+n) onto every rank
 void readRange(QuregImpl& q, i64 start, real* re, real* im, i64 n);
 

@@ -129,3 +129,35 @@ def qasm_log(env):
 
 SCENARIOS = {f.__name__: f for f in (random_ops_statevector, random_ops_density, measurement_and_collapse,
                                      calculations, qasm_log)}
+
+
+def checkpoint_save(env):
+    """Build a state and write a checkpoint to $QA_CKPT (any rank count)."""
+    import os
+
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+
+    r = qa.Register(env, 11)
+    r.init_plus()
+    random_layered(11, 3, seed=9).apply(r)
+    assert r.save(os.environ["QA_CKPT"])
+    out = {"state": r.to_numpy()}
+    r.close()
+    return out
+
+
+def checkpoint_load(env):
+    """Restore the checkpoint at $QA_CKPT (written by any rank count)."""
+    import os
+
+    import quest_amd as qa
+
+    r = qa.Register(env, 11)
+    assert r.load(os.environ["QA_CKPT"])
+    out = {"state": r.to_numpy()}
+    r.close()
+    return out
+
+
+SCENARIOS.update({f.__name__: f for f in (checkpoint_save, checkpoint_load)})

@@ -350,3 +350,23 @@ def test_reference_golden_suite_fp32_on_gpu():
                          timeout=600)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "773 passed, 0 failed" in out.stdout
+
+
+def test_checkpoint_round_trip_gpu(genv, tmp_path):
+    """Binary checkpoint of a 24-qubit register (256 MiB) through host slices."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+
+    r = qa.Register(genv, 24)
+    r.init_plus()
+    random_layered(24, 2, seed=2).apply(r)
+    want_p = [r.prob(q, 1) for q in (0, 11, 23)]
+    amp = r.amp(12345)
+    assert r.save(tmp_path / "ck")
+    s = qa.Register(genv, 24)
+    assert s.load(tmp_path / "ck")
+    assert [s.prob(q, 1) for q in (0, 11, 23)] == want_p
+    assert s.amp(12345) == amp
+    assert abs(s.inner(r) - 1) < 1e-12
+    r.close()
+    s.close()
