@@ -44,11 +44,50 @@ void setNoDelay(int fd) {
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
 }
 
+// Failure detection: a peer that makes no progress for QUEST_COMM_TIMEOUT
+// seconds (default 900; 0 = wait forever) is reported and this rank exits,
+// instead of the whole job hanging on a dead or stuck rank.
+int timeoutMs() {
+    static const int ms = [] {
+        const char* e = getenv("QUEST_COMM_TIMEOUT");
+        const double sec = e ? atof(e) : 900.0;
+        return sec <= 0 ? -1 : (int)(sec * 1000.0);
+    }();
+    return ms;
+}
+
+int peerOf(int fd) {
+    for (int r = 0; r < (int)g_fd.size(); r++)
+        if (g_fd[r] == fd) return r;
+    return -1;
+}
+
+// wait until fd is ready for `events`; exits on timeout
+short waitFd(int fd, short events) {
+    for (;;) {
+        pollfd p{fd, events, 0};
+        const int rc = poll(&p, 1, timeoutMs());
+        if (rc < 0) {
+            if (errno == EINTR) continue;
+            die("poll");
+        }
+        if (rc == 0) {
+            fprintf(stderr,
+                    "QuEST socket comm error (rank %d): no progress from peer rank %d for %.0f s "
+                    "(QUEST_COMM_TIMEOUT); giving up\n",
+                    g_rank, peerOf(fd), timeoutMs() / 1000.0);
+            exit(EXIT_FAILURE);
+        }
+        return p.revents;
+    }
+}
+
 void blockingWrite(int fd, const void* b, size_t n) {
     const char* p = (const char*)b;
     while (n) {
-        ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
-        if (k < 0 && (errno == EINTR || errno == EAGAIN)) continue;
+        waitFd(fd, POLLOUT);
+        ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL | MSG_DONTWAIT);
+        if (k < 0 && (errno == EINTR || errno == EAGAIN || errno == EWOULDBLOCK)) continue;
         if (k <= 0) die("send");
         p += k;
         n -= (size_t)k;
@@ -58,9 +97,11 @@ void blockingWrite(int fd, const void* b, size_t n) {
 void blockingRead(int fd, void* b, size_t n) {
     char* p = (char*)b;
     while (n) {
-        ssize_t k = ::recv(fd, p, n, 0);
-        if (k < 0 && (errno == EINTR || errno == EAGAIN)) continue;
-        if (k <= 0) die("recv");
+        waitFd(fd, POLLIN);
+        ssize_t k = ::recv(fd, p, n, MSG_DONTWAIT);
+        if (k < 0 && (errno == EINTR || errno == EAGAIN || errno == EWOULDBLOCK)) continue;
+        if (k == 0) die("peer closed the connection");
+        if (k < 0) die("recv");
         p += k;
         n -= (size_t)k;
     }
@@ -73,22 +114,19 @@ void duplex(int fd, const void* sbuf, void* rbuf, size_t n) {
     char* r = (char*)rbuf;
     size_t sent = 0, got = 0;
     while (sent < n || got < n) {
-        pollfd p{fd, 0, 0};
-        if (sent < n) p.events |= POLLOUT;
-        if (got < n) p.events |= POLLIN;
-        if (poll(&p, 1, -1) < 0) {
-            if (errno == EINTR) continue;
-            die("poll");
-        }
-        if ((p.revents & POLLOUT) && sent < n) {
+        short ev = 0;
+        if (sent < n) ev |= POLLOUT;
+        if (got < n) ev |= POLLIN;
+        const short rev = waitFd(fd, ev);
+        if ((rev & POLLOUT) && sent < n) {
             ssize_t k = ::send(fd, s + sent, n - sent, MSG_NOSIGNAL | MSG_DONTWAIT);
             if (k > 0) sent += (size_t)k;
             else if (k < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) die("send");
         }
-        if ((p.revents & (POLLIN | POLLHUP | POLLERR)) && got < n) {
+        if ((rev & (POLLIN | POLLHUP | POLLERR)) && got < n) {
             ssize_t k = ::recv(fd, r + got, n - got, MSG_DONTWAIT);
             if (k > 0) got += (size_t)k;
-            else if (k == 0) die("peer closed");
+            else if (k == 0) die("peer closed the connection");
             else if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) die("recv");
         }
     }
@@ -138,6 +176,7 @@ void init(int rank, int size) {
         g_fd[j] = fd;
     }
     for (int k = rank + 1; k < size; k++) {
+        waitFd(ls, POLLIN);  // a rank that never connects times out here
         int fd = accept(ls, nullptr, nullptr);
         if (fd < 0) die("accept");
         setNoDelay(fd);

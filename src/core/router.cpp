@@ -8,6 +8,7 @@
 
 #include "../comm/comm.hpp"
 #include "backend.hpp"
+#include "trace.hpp"
 
 namespace qa {
 
@@ -69,6 +70,9 @@ void enqueue(QuregImpl& q, const Op& op) {
 void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     if (k <= 0) return;
     be::flush(q);
+    trace::Range range("quest.swap");
+    const double t0 = trace::now();
+    const long long bytes0 = stats().bytesExchanged;
     // order by rank bit so that peers come in increasing (peer ^ rank) order
     int gpos[8], lpos[8], idx[8];
     for (int m = 0; m < k; m++) idx[m] = m;
@@ -119,6 +123,9 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         q.p2l[l] = lg;
     }
     stats().swaps += k;
+    if (trace::on())
+        trace::event("swap", "\"k\": %d, \"bytes_sent\": %lld, \"host_ms\": %.3f", k,
+                     stats().bytesExchanged - bytes0, 1e3 * (trace::now() - t0));
 }
 
 u64 logicalTargets(const Op& op) {
@@ -256,10 +263,14 @@ void create(QuregImpl& q, int nSV, bool density) {
     q.numAmpsPerChunk = (i64)1 << q.L;
     resetLayout(q);
     be::allocState(q);
+    if (trace::on())
+        trace::event("create", "\"qubits\": %d, \"density\": %d, \"local_qubits\": %d, \"ranks\": %d", nSV,
+                     density ? 1 : 0, q.L, q.numChunks);
 }
 
 void destroy(QuregImpl& q) {
     drain(q);
+    if (trace::on()) trace::event("destroy", "\"qubits\": %d", q.nSV);
     be::freeState(q);
 }
 

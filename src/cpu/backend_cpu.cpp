@@ -14,6 +14,7 @@
 #include "../core/backend.hpp"
 #include "../core/router.hpp"
 #include "../core/tiles.hpp"
+#include "../core/trace.hpp"
 
 namespace qa {
 namespace be {
@@ -351,8 +352,12 @@ void enqueue(QuregImpl& q, const Op& op) {
 
 void flush(QuregImpl& q) {
     if (q.pending.empty()) return;
+    const size_t opsIn = q.pending.size();
     TileProgram prog;
     planTiles(q.pending, q.L, fuseQubits(), 4, rt().fusion, prog);
+    if (trace::on())
+        trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
+                     q.pending.size(), prog.passes.size());
     // QUEST_CPU_PLANNER: 0 op by op, 1 register phases, 2 dense blocks (default)
     static const int planner = [] {
         const char* e = getenv("QUEST_CPU_PLANNER");

@@ -14,6 +14,7 @@
 #include "../core/backend.hpp"
 #include "../core/router.hpp"
 #include "qa_hip.h"
+#include "../core/trace.hpp"
 
 namespace qa {
 namespace hipk {
@@ -243,12 +244,17 @@ void enqueue(QuregImpl& q, const Op& op) {
 
 void flush(QuregImpl& q) {
     if (q.pending.empty()) return;
+    trace::Range range("quest.flush");
+    const size_t opsIn = q.pending.size();
     TileProgram prog;
     planTiles(q.pending, q.L, tileQubits(q.L), sizeof(real) == 8 ? 4 : 5, rt().fusion, prog);
     if (tuning().tileMode == 1)
         planPhases(prog, kTileQubits, kRegSlots);
     else if (tuning().tileMode == 2)
         planDenseBlocks(prog, kTileQubits, kRegSlots);
+    if (trace::on())
+        trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
+                     q.pending.size(), prog.passes.size());
     std::vector<Op> src;
     src.swap(q.pending);
     runProgram(q, src, prog);

@@ -161,3 +161,20 @@ def checkpoint_load(env):
 
 
 SCENARIOS.update({f.__name__: f for f in (checkpoint_save, checkpoint_load)})
+
+
+def hang_rank1(env):
+    """Rank 1 stops responding; rank 0 must give up after QUEST_COMM_TIMEOUT."""
+    import time
+
+    import quest_amd as qa
+
+    r = qa.Register(env, 8)
+    r.init_plus()
+    if env.rank == 1:
+        time.sleep(120)
+    p = r.total_prob()
+    return {"p": p}
+
+
+SCENARIOS["hang_rank1"] = hang_rank1
