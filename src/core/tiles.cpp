@@ -53,6 +53,7 @@ void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k,
             t.m[2 * j] = op.m[j].re;
             t.m[2 * j + 1] = op.m[j].im;
         }
+        laneSwaps(t, n);
         out.ops.push_back(t);
     }
     ps.opEnd = (int)out.ops.size();
@@ -60,6 +61,78 @@ void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k,
 }
 
 }  // namespace
+
+namespace {
+unsigned insertZero(unsigned x, int b) { return ((x >> b) << (b + 1)) | (x & ((1u << b) - 1u)); }
+
+void fillUniformParts(TileOp& op) {
+    const int nt = op.kind == (int)OpKind::Mat2 ? 1 : op.kind == (int)OpKind::Mat4 ? 2 : 0;
+    int lo = op.t[0], hi = op.t[0];
+    if (nt == 2) {
+        lo = std::min(op.t[0], op.t[1]);
+        hi = std::max(op.t[0], op.t[1]);
+    }
+    for (int u = 0; u < 16; u++) {
+        unsigned p = 256u * (unsigned)u;
+        if (nt >= 1) p = insertZero(p, lo);
+        if (nt == 2) p = insertZero(p, hi);
+        for (int s = 0; s < op.nsw; s++) {
+            const unsigned a = op.swA[s], b = op.swB[s];
+            const unsigned x = ((p >> a) ^ (p >> b)) & 1u;
+            p ^= (x << a) | (x << b);
+        }
+        op.du[u] = p;
+        op.sdu[u] = ldsSwizzle(p);
+    }
+}
+}  // namespace
+
+void laneSwaps(TileOp& op, int k) {
+    op.nsw = 0;
+    if (op.kind != (int)OpKind::Mat2 && op.kind != (int)OpKind::Mat4) {
+        fillUniformParts(op);
+        return;
+    }
+    const int nt = op.kind == (int)OpKind::Mat2 ? 1 : 2;
+    unsigned tmask = 0;
+    for (int i = 0; i < nt; i++) tmask |= 1u << op.t[i];
+    int map[32], nf = 0;  // work-item bit i -> element bit map[i]
+    for (int b = 0; b < k; b++)
+        if (!((tmask >> b) & 1)) map[nf++] = b;
+    // GF(2) basis with distinct leading bits: reduce v against it (largest first)
+    auto reduce = [](const std::vector<unsigned>& basis, unsigned v) {
+        std::vector<unsigned> b = basis;
+        std::sort(b.rbegin(), b.rend());
+        for (unsigned x : b) v = std::min(v, v ^ x);
+        return v;
+    };
+    auto indep = [&](std::vector<unsigned>& basis, unsigned v) { return reduce(basis, v) != 0; };
+    std::vector<unsigned> bR, bW;
+    for (int i = 0; i < 5 && i < nf; i++) {
+        auto fits = [&](int e) {
+            const unsigned r = ldsSwizzle(1u << e) & 31u, w = ldsSwizzle(1u << e) & 15u;
+            return indep(bR, r) && (i >= 4 || indep(bW, w));
+        };
+        if (!fits(map[i])) {
+            int j = -1;
+            for (int c = i + 1; c < nf; c++)
+                if (fits(map[c])) {
+                    j = c;
+                    break;
+                }
+            if (j < 0 || op.nsw == 4) continue;  // best effort
+            op.swA[op.nsw] = (unsigned char)map[i];
+            op.swB[op.nsw] = (unsigned char)map[j];
+            op.nsw++;
+            std::swap(map[i], map[j]);
+        }
+        const unsigned v = ldsSwizzle(1u << map[i]);
+        const unsigned r = reduce(bR, v & 31u), w = reduce(bW, v & 15u);
+        if (r) bR.push_back(r);
+        if (i < 4 && w) bW.push_back(w);
+    }
+    fillUniformParts(op);
+}
 
 namespace {
 

@@ -27,10 +27,24 @@ struct TileOp {
     int t[4];            // tile-local target bits
     int rt[4];           // register slots of the targets inside a register phase
     unsigned ctrlIn;     // tile-local mask of bits that must be 1
-    unsigned pad;
+    int nsw;             // element-bit swaps applied to the work-item index (below)
+    unsigned char swA[4], swB[4];
+    unsigned du[16];     // element of work item 256 u (u < 16), after insertion + swaps
+    unsigned sdu[16];    // ldsSwizzle(du[u])
     u64 ctrlOut;         // physical bits outside the tile that must be 1
     real m[32];          // matrix, interleaved re/im, row-major
 };
+
+// GPU op-by-op LDS access: work item j of an op (a pair / quad / element) is
+// expanded to tile element p by inserting zeros at the target bits; the
+// first 5 bits of j then come from the lowest free bits.  When targets sit
+// low, those give 32 lanes colliding LDS slots under ldsSwizzle.  The host
+// records up to 4 element-bit swaps (swA[i] <-> swB[i], applied to p in
+// order) that re-map lane bits 0-4 to free bits with independent slot
+// vectors (reads: 32-lane groups, slot = 8-byte word mod 32; writes: 16-lane
+// groups, mod 16), making every access of the op conflict-free.
+// Also fills du / sdu, the wave-uniform parts of the work-item addresses.
+void laneSwaps(TileOp& op, int k);
 
 // A phase of a pass: a run of ops executed with each thread holding 2^R
 // amplitudes in registers, namely the tile elements spanned by the R tile

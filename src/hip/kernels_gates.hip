@@ -53,6 +53,20 @@ __device__ __forceinline__ unsigned li(unsigned p) {
 // ops applied directly on the LDS tile (generic kernel, and fallback phases)
 // ---------------------------------------------------------------------------
 
+// host-chosen element-bit swaps that make the op's lane -> element map free
+// of LDS bank conflicts under the swizzle (tiles.hpp: laneSwaps)
+template <bool SW>
+__device__ __forceinline__ unsigned laneMap(unsigned p, const TileOp& op) {
+    if constexpr (SW) {
+        for (int s = 0; s < op.nsw; s++) {
+            const unsigned a = op.swA[s], b = op.swB[s];
+            const unsigned x = ((p >> a) ^ (p >> b)) & 1u;
+            p ^= (x << a) | (x << b);
+        }
+    }
+    return p;
+}
+
 template <typename T, bool SW>
 __device__ __forceinline__ void applyMat2(T* __restrict__ sre, T* __restrict__ sim, unsigned n, const TileOp& op) {
     const int t = op.t[0];
@@ -60,7 +74,7 @@ __device__ __forceinline__ void applyMat2(T* __restrict__ sre, T* __restrict__ s
     const T m0r = (T)op.m[0], m0i = (T)op.m[1], m1r = (T)op.m[2], m1i = (T)op.m[3];
     const T m2r = (T)op.m[4], m2i = (T)op.m[5], m3r = (T)op.m[6], m3i = (T)op.m[7];
     for (unsigned j = threadIdx.x; j < (n >> 1); j += blockDim.x) {
-        const unsigned p0 = ins0(j, t);
+        const unsigned p0 = laneMap<SW>(ins0(j, t), op);
         if ((p0 & cin) != cin) continue;
         const unsigned a0 = li<SW>(p0), a1 = li<SW>(p0 | (1u << t));
         const T r0 = sre[a0], i0 = sim[a0], r1 = sre[a1], i1 = sim[a1];
@@ -90,7 +104,7 @@ __device__ __forceinline__ void applyMat4(T* __restrict__ sre, T* __restrict__ s
     const int lo = a < b ? a : b, hi = a < b ? b : a;
     const unsigned cin = op.ctrlIn;
     for (unsigned j = threadIdx.x; j < (n >> 2); j += blockDim.x) {
-        const unsigned p = ins0(ins0(j, lo), hi);
+        const unsigned p = laneMap<SW>(ins0(ins0(j, lo), hi), op);
         if ((p & cin) != cin) continue;
         unsigned idx[4];
         T vr[4], vi[4];
@@ -163,6 +177,104 @@ __device__ __forceinline__ void applyLdsOp(T* sre, T* sim, unsigned n, const Til
         case OpKind::Diag: applyDiag<T, SW>(sre, sim, n, op); break;
         case OpKind::Mat4: applyMat4<T, SW>(sre, sim, n, op); break;
         case OpKind::DensChan2: applyDensChan2<T, SW>(sre, sim, n, op); break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ops on the swizzled tile of the compile-time kernel (N elements, 256
+// threads).  Work item j = tid + 256 u of an op maps to element
+// laneMap(ins0(.., targets)) and then to LDS word swz(.): every step is a
+// bit permutation or XOR-linear, so the word of item u, member g is
+//     swz(map(tid)) ^ swz(map(256 u) | g-bits)
+// -- one per-thread base plus a wave-uniform (scalar) term: a single v_xor
+// per access instead of recomputing the insertion and the swizzle.
+// ---------------------------------------------------------------------------
+
+template <typename T, unsigned N>
+__device__ __forceinline__ void mat2Tile(T* __restrict__ sre, T* __restrict__ sim, const TileOp& op) {
+    constexpr int P = N / 2 / 256;
+    static_assert(P <= 16, "TileOp::du holds 16 work-item groups");
+    const int t = op.t[0];
+    const unsigned cin = op.ctrlIn;
+    const T m0r = (T)op.m[0], m0i = (T)op.m[1], m1r = (T)op.m[2], m1i = (T)op.m[3];
+    const T m2r = (T)op.m[4], m2i = (T)op.m[5], m3r = (T)op.m[6], m3i = (T)op.m[7];
+    const unsigned p0 = laneMap<true>(ins0(threadIdx.x, t), op);
+    const unsigned a0 = swz(p0);
+    const unsigned tb = swz(1u << t);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+        const unsigned du = op.du[u];  // uniform, precomputed on the host
+        if (((p0 ^ du) & cin) != cin) continue;
+        const unsigned i0 = a0 ^ op.sdu[u], i1 = i0 ^ tb;
+        const T r0 = sre[i0], im0 = sim[i0], r1 = sre[i1], im1 = sim[i1];
+        sre[i0] = m0r * r0 - m0i * im0 + m1r * r1 - m1i * im1;
+        sim[i0] = m0r * im0 + m0i * r0 + m1r * im1 + m1i * r1;
+        sre[i1] = m2r * r0 - m2i * im0 + m3r * r1 - m3i * im1;
+        sim[i1] = m2r * im0 + m2i * r0 + m3r * im1 + m3i * r1;
+    }
+}
+
+template <typename T, unsigned N>
+__device__ __forceinline__ void mat4Tile(T* __restrict__ sre, T* __restrict__ sim, const TileOp& op) {
+    constexpr int P = N / 4 / 256;
+    static_assert(P <= 16, "TileOp::du holds 16 work-item groups");
+    const int a = op.t[0], b = op.t[1];
+    const int lo = a < b ? a : b, hi = a < b ? b : a;
+    const unsigned cin = op.ctrlIn;
+    const unsigned p0 = laneMap<true>(ins0(ins0(threadIdx.x, lo), hi), op);
+    const unsigned a0 = swz(p0);
+    const unsigned ga = swz(1u << a), gb = swz(1u << b);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+        const unsigned du = op.du[u];  // uniform, precomputed on the host
+        if (((p0 ^ du) & cin) != cin) continue;
+        const unsigned b0 = a0 ^ op.sdu[u];
+        const unsigned idx[4] = {b0, b0 ^ ga, b0 ^ gb, b0 ^ ga ^ gb};
+        T vr[4], vi[4];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            vr[g] = sre[idx[g]];
+            vi[g] = sim[idx[g]];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            T sr = 0, si = 0;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const T mr = (T)op.m[2 * (4 * r + c)], mi = (T)op.m[2 * (4 * r + c) + 1];
+                sr += mr * vr[c] - mi * vi[c];
+                si += mr * vi[c] + mi * vr[c];
+            }
+            sre[idx[r]] = sr;
+            sim[idx[r]] = si;
+        }
+    }
+}
+
+template <typename T, unsigned N>
+__device__ __forceinline__ void diagTile(T* __restrict__ sre, T* __restrict__ sim, const TileOp& op) {
+    constexpr int P = N / 256;
+    const unsigned cin = op.ctrlIn;
+    const T tr = (T)op.m[0], ti = (T)op.m[1];
+    const unsigned a0 = swz(threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+        const unsigned p = threadIdx.x + 256u * u;
+        if ((p & cin) != cin) continue;
+        const unsigned i = a0 ^ swz(256u * u);  // compile-time constant
+        const T r = sre[i], im = sim[i];
+        sre[i] = tr * r - ti * im;
+        sim[i] = tr * im + ti * r;
+    }
+}
+
+template <typename T, unsigned N>
+__device__ __forceinline__ void applyTileOp(T* sre, T* sim, const TileOp& op) {
+    switch ((OpKind)op.kind) {
+        case OpKind::Mat2: mat2Tile<T, N>(sre, sim, op); break;
+        case OpKind::Diag: diagTile<T, N>(sre, sim, op); break;
+        case OpKind::Mat4: mat4Tile<T, N>(sre, sim, op); break;
+        case OpKind::DensChan2: applyDensChan2<T, true>(sre, sim, N, op); break;
     }
 }
 
@@ -537,7 +649,7 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
                     for (int o = ph.opBegin; o < ph.opEnd; o++) {
                         const TileOp& op = ops[o];
                         if (((unsigned long long)base & op.ctrlOut) != op.ctrlOut) continue;
-                        applyLdsOp<T, true>(sre, sim, N, op);
+                        applyTileOp<T, N>(sre, sim, op);
                         __syncthreads();
                     }
                 } else if constexpr (MODE == 2) {
@@ -552,7 +664,7 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
             for (int o = 0; o < a.nOps; o++) {
                 const TileOp& op = ops[o];
                 if (((unsigned long long)base & op.ctrlOut) != op.ctrlOut) continue;
-                applyLdsOp<T, true>(sre, sim, N, op);
+                applyTileOp<T, N>(sre, sim, op);
                 __syncthreads();
             }
         }
