@@ -22,7 +22,8 @@ Runs on whatever backend and rank layout the process has (every rank runs
 every case; distributed runs exercise the exchange paths with 3-qubit
 registers spread over 2-4 ranks, like the reference's ``mpiexec -n 4``).
 
-    python -m quest_amd.utils.golden [--filter hadamard] [--tol 1e-10]
+    python -m quest_amd.utils.golden [--filter hadamard] [--tol 1e-10] [--log out]
+    python -m quest_amd.utils.golden --generate new.json   # expectations from this build
 """
 from __future__ import annotations
 
@@ -137,6 +138,71 @@ def run_case(capi, env, func: str, case: dict, tol: float) -> list[str]:
     return errs
 
 
+def observe_case(capi, env, func: str, case: dict) -> dict:
+    """Run a case and return what this build produces, in the case's own
+    schema ("returns" or "expect" with the case's P/M/S checks): the
+    reference runner's golden-generation mode (QuESTCore.py:584-711)."""
+    import numpy as np
+
+    q = _make_register(capi, env, case)
+    try:
+        fn = getattr(capi, func)
+        args = _convert_args(func, case["args"])
+        if "returns" in case:
+            got = fn(q, *args)
+            if isinstance(got, complex):
+                return {"returns": [got.real, got.imag]}
+            return {"returns": got}
+        fn(q, *args)
+        exp = {}
+        for chk in (case.get("checks") or "S"):
+            if chk in "Pp":
+                exp["P"] = capi.calcTotalProb(q)
+            elif chk in "Mm":
+                exp["M"] = [[capi.calcProbOfOutcome(q, b, 0), capi.calcProbOfOutcome(q, b, 1)]
+                            for b in range(case["n"])]
+            elif chk in "Ss":
+                amps = capi.getAmps(q, 0, q.numAmpsTotal)
+                exp["S"] = [[float(a.real), float(a.imag)] for a in np.asarray(amps)]
+        return {"expect": exp}
+    finally:
+        capi.destroyQureg(q, env)
+
+
+def generate(out_path: str, env=None, path: str = DEFAULT_DATA, filt: str | None = None) -> int:
+    """Write a copy of the golden data whose expectations come from this
+    build (regression baselines for new cases or other precisions)."""
+    from ..ops import capi
+
+    with open(path) as f:
+        data = json.load(f)
+    own_env = env is None
+    if own_env:
+        env = capi.createQuESTEnv()
+    n = 0
+    try:
+        for name, suite in data["suites"].items():
+            if filt and filt not in name:
+                continue
+            for case in suite["cases"]:
+                nsv = case["n"] * (2 if case["density"] else 1)
+                if (1 << nsv) < 2 * env.numRanks:
+                    continue
+                obs = observe_case(capi, env, suite["function"], case)
+                case.pop("returns", None)
+                case.pop("expect", None)
+                case.update(obs)
+                n += 1
+        data["source"] = "generated by quest_amd.utils.golden --generate"
+        if env.rank == 0:
+            with open(out_path, "w") as f:
+                json.dump(data, f, separators=(",", ":"))
+    finally:
+        if own_env:
+            capi.destroyQuESTEnv(env)
+    return n
+
+
 def run_all(env=None, filt: str | None = None, tol: float = 1e-10, path: str = DEFAULT_DATA,
             verbose: bool = False) -> tuple[int, list[str]]:
     from ..ops import capi
@@ -174,15 +240,26 @@ def main(argv=None):
     ap.add_argument("--tol", type=float, default=1e-10)
     ap.add_argument("--data", default=DEFAULT_DATA)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--generate", metavar="OUT", default=None,
+                    help="write the data with expectations produced by this build to OUT")
+    ap.add_argument("--log", metavar="FILE", default=None, help="also write results to FILE.<rank>")
     args = ap.parse_args(argv)
     from ..ops import capi
 
     env = capi.createQuESTEnv()
+    if args.generate:
+        n = generate(args.generate, env, args.data, args.filter)
+        if env.rank == 0:
+            print(f"generated {n} cases -> {args.generate}")
+        capi.destroyQuESTEnv(env)
+        return 0
     passed, failures = run_all(env, args.filter, args.tol, args.data, args.verbose)
+    lines = [f"FAIL {f}" for f in failures] + [f"{passed} passed, {len(failures)} failed"]
     if env.rank == 0:
-        for f in failures:
-            print("FAIL", f)
-        print(f"{passed} passed, {len(failures)} failed")
+        print("\n".join(lines))
+    if args.log:
+        with open(f"{args.log}.{env.rank}", "w") as f:
+            f.write("\n".join(lines) + "\n")
     capi.destroyQuESTEnv(env)
     return 1 if failures else 0
 

@@ -195,3 +195,21 @@ def test_rotate_round_trip_and_normalisation(env):
         capi.compactUnitary(mq, t, alpha_b, beta_b)
     assert capi.calcTotalProb(mq) == pytest.approx(1.0, abs=1e-10)
     capi.destroyQureg(mq, env.env)
+
+
+def test_golden_generate_roundtrip(env, tmp_path):
+    """--generate writes data whose expectations this build then passes
+    (the reference runner's -g mode); generated values match the originals."""
+    import json
+
+    from quest_amd.utils import golden
+
+    out = tmp_path / "gen.json"
+    n = golden.generate(str(out), env.env, filt="unit/state_vector/gates/hadamard")
+    assert n == 12
+    passed, failures = golden.run_all(env.env, path=str(out))
+    assert not failures and passed == 12
+    a = json.load(open(out))["suites"]["unit/state_vector/gates/hadamard.test"]["cases"]
+    b = golden.load_suites()["unit/state_vector/gates/hadamard.test"]["cases"]
+    for x, y in zip(a, b):
+        assert x["expect"]["P"] == pytest.approx(y["expect"]["P"], abs=1e-10)

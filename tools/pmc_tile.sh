@@ -1,3 +1,5 @@
+# rocprofv3 kernel trace + two PMC passes of the fused tile kernel on tools/tile_workload.py
+# (run on the GPU box: bash tools/pmc_tile.sh; results under gpurun_out/pmc_*)
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/pmc_t -o run --output-format csv -- python3 $R/tools/tile_workload.py > $R/gpurun_out/pmc_t.log 2>&1 &&
