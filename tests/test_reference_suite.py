@@ -207,7 +207,7 @@ def test_golden_generate_roundtrip(env, tmp_path):
     out = tmp_path / "gen.json"
     n = golden.generate(str(out), env.env, filt="unit/state_vector/gates/hadamard")
     assert n == 12
-    passed, failures = golden.run_all(env.env, path=str(out))
+    passed, failures = golden.run_all(env.env, filt="unit/state_vector/gates/hadamard", path=str(out))
     assert not failures and passed == 12
     a = json.load(open(out))["suites"]["unit/state_vector/gates/hadamard.test"]["cases"]
     b = golden.load_suites()["unit/state_vector/gates/hadamard.test"]["cases"]
