@@ -80,10 +80,10 @@ __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* _
             const long long u = u0 + k * step;
             up[k] = u < units ? insertAll(u * VN, ib) : -1;
             if (up[k] >= 0) {
-                ar[k] = *reinterpret_cast<const V*>(re + up[k]);
-                ai[k] = *reinterpret_cast<const V*>(im + up[k]);
-                br[k] = *reinterpret_cast<const V*>(re + up[k] + tbit);
-                bi[k] = *reinterpret_cast<const V*>(im + up[k] + tbit);
+                ar[k] = streamLoad(reinterpret_cast<const V*>(re + up[k]));
+                ai[k] = streamLoad(reinterpret_cast<const V*>(im + up[k]));
+                br[k] = streamLoad(reinterpret_cast<const V*>(re + up[k] + tbit));
+                bi[k] = streamLoad(reinterpret_cast<const V*>(im + up[k] + tbit));
             }
         }
 #pragma unroll
@@ -98,10 +98,10 @@ __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* _
                 if ((((unsigned)up[k] + e) & ib.predMask) != ib.predMask) continue;
                 mat2apply(m, pr[e], pi[e], qr[e], qi[e]);
             }
-            *reinterpret_cast<V*>(re + up[k]) = ar[k];
-            *reinterpret_cast<V*>(im + up[k]) = ai[k];
-            *reinterpret_cast<V*>(re + up[k] + tbit) = br[k];
-            *reinterpret_cast<V*>(im + up[k] + tbit) = bi[k];
+            streamStore(reinterpret_cast<V*>(re + up[k]), ar[k]);
+            streamStore(reinterpret_cast<V*>(im + up[k]), ai[k]);
+            streamStore(reinterpret_cast<V*>(re + up[k] + tbit), br[k]);
+            streamStore(reinterpret_cast<V*>(im + up[k] + tbit), bi[k]);
         }
     });
 }
@@ -121,8 +121,8 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
             const long long u = u0 + k * step;
             at[k] = u < units ? insertAll(u * VN, ib) : -1;
             if (at[k] >= 0) {
-                vr[k] = *reinterpret_cast<const V*>(re + at[k]);
-                vi[k] = *reinterpret_cast<const V*>(im + at[k]);
+                vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
+                vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
             }
         }
 #pragma unroll
@@ -137,8 +137,8 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
                 const int f = e | (1 << t);
                 mat2apply(m, pr[e], pi[e], pr[f], pi[f]);
             }
-            *reinterpret_cast<V*>(re + at[k]) = vr[k];
-            *reinterpret_cast<V*>(im + at[k]) = vi[k];
+            streamStore(reinterpret_cast<V*>(re + at[k]), vr[k]);
+            streamStore(reinterpret_cast<V*>(im + at[k]), vi[k]);
         }
     });
 }
@@ -158,8 +158,8 @@ __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* _
             const long long u = u0 + k * step;
             at[k] = u < units ? insertAll(u * VN, ib) : -1;
             if (at[k] >= 0) {
-                vr[k] = *reinterpret_cast<const V*>(re + at[k]);
-                vi[k] = *reinterpret_cast<const V*>(im + at[k]);
+                vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
+                vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
             }
         }
 #pragma unroll
@@ -174,8 +174,8 @@ __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* _
                 pr[e] = tr * a - ti * b;
                 pi[e] = tr * b + ti * a;
             }
-            *reinterpret_cast<V*>(re + at[k]) = vr[k];
-            *reinterpret_cast<V*>(im + at[k]) = vi[k];
+            streamStore(reinterpret_cast<V*>(re + at[k]), vr[k]);
+            streamStore(reinterpret_cast<V*>(im + at[k]), vi[k]);
         }
     });
 }

@@ -624,8 +624,8 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
     long long base = tileBaseOf(tile);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        rr[u] = *reinterpret_cast<const V*>(re + base + off[u]);
-        ri[u] = *reinterpret_cast<const V*>(im + base + off[u]);
+        rr[u] = streamLoad(reinterpret_cast<const V*>(re + base + off[u]));
+        ri[u] = streamLoad(reinterpret_cast<const V*>(im + base + off[u]));
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -639,8 +639,8 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
         const long long nbase = next < a.numTiles ? tileBaseOf(next) : base;
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            rr[u] = *reinterpret_cast<const V*>(re + nbase + off[u]);
-            ri[u] = *reinterpret_cast<const V*>(im + nbase + off[u]);
+            rr[u] = streamLoad(reinterpret_cast<const V*>(re + nbase + off[u]));
+            ri[u] = streamLoad(reinterpret_cast<const V*>(im + nbase + off[u]));
         }
         if constexpr (PHASES) {
             for (int h = 0; h < a.nPhases; h++) {
@@ -671,8 +671,8 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const unsigned p = (threadIdx.x + 256u * u) * VN;
-            *reinterpret_cast<V*>(re + base + off[u]) = ldsGetVec<T>(sre, p);
-            *reinterpret_cast<V*>(im + base + off[u]) = ldsGetVec<T>(sim, p);
+            streamStore(reinterpret_cast<V*>(re + base + off[u]), ldsGetVec<T>(sre, p));
+            streamStore(reinterpret_cast<V*>(im + base + off[u]), ldsGetVec<T>(sim, p));
         }
         __syncthreads();
 #pragma unroll

@@ -48,6 +48,52 @@ struct Vec16<float> {
     static constexpr int n = 4;
 };
 
+#ifdef __HIPCC__
+// HBM streaming of the state: every amplitude is read and written once per
+// pass, so the accesses are marked non-temporal (QA_NONTEMPORAL=0 at build
+// time: plain accesses)
+#ifndef QA_NONTEMPORAL
+#define QA_NONTEMPORAL 1
+#endif
+typedef double qa_nd2 __attribute__((ext_vector_type(2)));
+typedef float qa_nf4 __attribute__((ext_vector_type(4)));
+template <typename V>
+struct NativeVec;
+template <>
+struct NativeVec<double2> {
+    using type = qa_nd2;
+};
+template <>
+struct NativeVec<float4> {
+    using type = qa_nf4;
+};
+
+template <typename V>
+__device__ __forceinline__ V streamLoad(const V* p) {
+#if QA_NONTEMPORAL
+    using N = typename NativeVec<V>::type;
+    const N n = __builtin_nontemporal_load(reinterpret_cast<const N*>(p));
+    V v;
+    __builtin_memcpy(&v, &n, sizeof v);
+    return v;
+#else
+    return *p;
+#endif
+}
+template <typename V>
+__device__ __forceinline__ void streamStore(V* p, V v) {
+#if QA_NONTEMPORAL
+    using N = typename NativeVec<V>::type;
+    N n;
+    __builtin_memcpy(&n, &v, sizeof n);
+    __builtin_nontemporal_store(n, reinterpret_cast<N*>(p));
+#else
+    *p = v;
+#endif
+}
+
+#endif  // __HIPCC__
+
 // Tile size of the compile-time tile kernel (2^K amplitudes, 256 threads x
 // 2^(K-8) registers): 32 KiB of LDS for fp64 and fp32 alike.
 constexpr int kTileQubits = sizeof(real) == 8 ? 11 : 12;
