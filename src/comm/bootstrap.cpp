@@ -76,8 +76,11 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
     memcpy(out + (size_t)rank * bytes, mine, bytes);
     if (size == 1) return;
 
+    // every rendezvous on its own port (base, base + 1, ...): a rank that
+    // finishes one early must not reach rank 0's previous listener
+    static int generation = 0;
     const std::string addr = hostAddress();
-    const int port = bootstrapPort();
+    const int port = bootstrapPort() + (generation++ % 8);
 
     if (rank == 0) {
         int ls = socket(AF_INET, SOCK_STREAM, 0);

@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../hip/qa_hip.h"
 #include "comm.hpp"
@@ -79,8 +80,8 @@ void sym(F& f, const char* name) {
     }
 }
 
-void loadRccl() {
-    if (R.lib) return;
+bool loadRccl() {
+    if (R.lib) return true;
     const char* env = getenv("QUEST_RCCL_LIB");
     const char* candidates[] = {env, "librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"};
     for (int i = 0; i < 4 && !R.lib; i++) {
@@ -92,7 +93,7 @@ void loadRccl() {
     }
     if (!R.lib) {
         fprintf(stderr, "QuEST: could not load librccl (%s)\n", dlerror());
-        exit(EXIT_FAILURE);
+        return false;
     }
     sym(R.getUniqueId, "ncclGetUniqueId");
     sym(R.commInitRank, "ncclCommInitRank");
@@ -106,6 +107,7 @@ void loadRccl() {
     sym(R.groupEnd, "ncclGroupEnd");
     sym(R.errorString, "ncclGetErrorString");
     sym(R.getVersion, "ncclGetVersion");
+    return true;
 }
 
 hipStream_t S() { return hipk::stream(); }
@@ -132,14 +134,36 @@ void init(int rank, int size) {
         sock::init(rank, size);
         return;
     }
-    loadRccl();
+    // RCCL unique id from rank 0; then every rank reports whether its
+    // communicator came up, and if any did not, all fall back together to
+    // the socket transport (staged through host memory) rather than hang
+    int ok = loadRccl() ? 1 : 0;
     ncclUniqueId id;
     memset(&id, 0, sizeof id);
-    if (rank == 0) QA_NCCL(R.getUniqueId(&id), "ncclGetUniqueId");
+    if (rank == 0 && ok && R.getUniqueId(&id) != ncclSuccess) ok = 0;
     std::string all((size_t)size * sizeof id, '\0');
     boot::allgather(rank, size, &id, &all[0], sizeof id);
     memcpy(&id, all.data(), sizeof id);  // rank 0's id
-    QA_NCCL(R.commInitRank(&g_comm, size, id, rank), "ncclCommInitRank");
+    std::vector<int> oks(size, 0);
+    boot::allgather(rank, size, &ok, oks.data(), sizeof(int));
+    for (int r = 0; r < size; r++) ok = ok && oks[r];  // rank 0 failing to make an id fails everyone
+    if (ok) {
+        const ncclResult_t rc = R.commInitRank(&g_comm, size, id, rank);
+        int mine = rc == ncclSuccess ? 1 : 0;
+        if (!mine) fprintf(stderr, "QuEST: ncclCommInitRank failed on rank %d: %s\n", rank, R.errorString(rc));
+        boot::allgather(rank, size, &mine, oks.data(), sizeof(int));
+        for (int r = 0; r < size; r++) ok = ok && oks[r];
+        if (!ok && mine) {
+            R.commDestroy(g_comm);
+            g_comm = nullptr;
+        }
+    }
+    if (!ok) {
+        if (rank == 0) fprintf(stderr, "QuEST: RCCL unavailable, using the socket transport (slow)\n");
+        g_socket = true;
+        sock::init(rank, size);
+        return;
+    }
     QA_HIP_CHECK(hipMalloc(&g_dScalars, sizeof(double) * 64));
     QA_HIP_CHECK(hipHostMalloc(&g_hScalars, sizeof(double) * 64, hipHostMallocDefault));
 }
