@@ -119,7 +119,8 @@ def main():
             "global_batch": 1,
             "seq_len": 1 << n,
             "gates_per_step": gates / max(args.steps, 1),
-            "parallelism": f"amplitude-sharded x{world} (RCCL swaps)",
+            "parallelism": f"dp{world}: amplitude-sharded over {world} GPU(s), qubit swaps over RCCL",
+            "transport": qa.capi.getQuESTTransport(),
             "fusion": not args.eager,
             "passes": stats["passes"],
             "swaps": stats["swaps"],

@@ -80,6 +80,8 @@ void resetQuESTStats(void);
 
 /* Name of the compiled backend: "HIP" (gfx950) or "CPU". */
 const char* getQuESTBackend(void);
+/* The inter-rank transport in use (RCCL / socket / single process). */
+const char* getQuESTTransport(void);
 
 /* Seed array used by seedQuESTDefault on this rank (after broadcast). */
 void getQuESTSeeds(unsigned long* seeds, int* numSeeds);

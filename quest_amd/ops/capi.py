@@ -143,7 +143,7 @@ class _Binding:
             "copyStateFromGPU": (v, [Q]), "copyChunkToBuffers": (v, [Q, C.c_void_p, C.c_void_p]),
             "copyChunkFromBuffers": (v, [Q, C.c_void_p, C.c_void_p]), "canonicaliseQureg": (v, [Q]),
             "getQubitLayout": (v, [Q, ip]), "getAmps": (v, [Q, ll, rp, rp, ll]), "getQuESTStats": (v, [P(QuESTStats)]), "resetQuESTStats": (v, []),
-            "getQuESTBackend": (C.c_char_p, []), "getQuESTSeeds": (v, [P(C.c_ulong), ip]),
+            "getQuESTBackend": (C.c_char_p, []), "getQuESTTransport": (C.c_char_p, []), "getQuESTSeeds": (v, [P(C.c_ulong), ip]),
             "saveQuregCheckpoint": (i, [Q, C.c_char_p]), "loadQuregCheckpoint": (i, [Q, C.c_char_p]),
         }
         for name, (res, args) in self.protos.items():
@@ -418,6 +418,10 @@ def setQuESTTuning(key: str, value: int) -> bool:
 
 def getQuESTBackend() -> str:
     return _call("getQuESTBackend").decode()
+
+
+def getQuESTTransport() -> str:
+    return _call("getQuESTTransport").decode()
 
 
 def saveQuregCheckpoint(q, path) -> bool:

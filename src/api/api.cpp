@@ -957,6 +957,12 @@ void getQuESTStats(QuESTStats* s) {
 
 void resetQuESTStats(void) { stats() = Stats(); }
 
+const char* getQuESTTransport(void) {
+    static std::string d;
+    d = comm::describe();
+    return d.c_str();
+}
+
 const char* getQuESTBackend(void) { return be::shortName(); }
 
 void getQuESTSeeds(unsigned long* seeds, int* numSeeds) {
