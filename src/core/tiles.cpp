@@ -362,10 +362,11 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
     order.reserve(n);
     std::vector<char> done(n, 0);
     int first = 0;
-    while ((int)order.size() < n) {
-        while (done[first]) first++;
-        const int begin = (int)order.size();
-        u64 high = 0;           // high tile bits claimed by this pass
+    std::vector<int> take, best;
+    // one greedy scan from `first` with the high bits `preset` claimed up front
+    auto scan = [&](u64 preset, std::vector<int>& picked) {
+        picked.clear();
+        u64 high = preset;
         u64 blockedTg = 0;      // targets of ops deferred past this pass
         u64 blockedTouch = 0;   // targets | controls of deferred ops
         for (int i = first; i < n; i++) {
@@ -376,14 +377,47 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             const u64 need = high | (tg & ~low);
             if (free && popcount64(need) <= highSlots) {
                 high = need;
-                order.push_back(ops[i]);
-                done[i] = 1;
+                picked.push_back(i);
             } else {
                 blockedTg |= tg;
                 blockedTouch |= touch;
             }
         }
-        emitPass(order, begin, (int)order.size(), high, L, k, c, out);
+        return high;
+    };
+    while ((int)order.size() < n) {
+        while (done[first]) first++;
+        const int begin = (int)order.size();
+        // candidates: plain in-order greedy, and greedy seeded with the high
+        // targets of one of the next few ops; keep the pass holding most ops
+        u64 bestHigh = scan(0, best);
+        static const int maxSeeds = [] {
+            const char* e = getenv("QUEST_PLAN_SEEDS");
+            return e ? atoi(e) : 24;
+        }();
+        int seeds = 0;
+        u64 tried[16];
+        int nTried = 0;
+        for (int i = first; i < n && seeds < maxSeeds; i++) {
+            if (done[i]) continue;
+            const u64 h = targetMask(ops[i]) & ~low;
+            if (!h) continue;
+            seeds++;
+            bool dup = false;
+            for (int t = 0; t < nTried; t++) dup |= tried[t] == h;
+            if (dup || nTried == 16) continue;
+            tried[nTried++] = h;
+            const u64 hh = scan(h, take);
+            if (take.size() > best.size()) {
+                best.swap(take);
+                bestHigh = hh;
+            }
+        }
+        for (int i : best) {
+            order.push_back(ops[i]);
+            done[i] = 1;
+        }
+        emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out);
     }
     ops.swap(order);
 }
