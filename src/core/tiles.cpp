@@ -65,7 +65,8 @@ void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k,
 namespace {
 unsigned insertZero(unsigned x, int b) { return ((x >> b) << (b + 1)) | (x & ((1u << b) - 1u)); }
 
-void fillUniformParts(TileOp& op) {
+void fillUniformParts(TileOp& op, int k) {
+    const unsigned th = tileThreads(k);
     const int nt = op.kind == (int)OpKind::Mat2 ? 1 : op.kind == (int)OpKind::Mat4 ? 2 : 0;
     int lo = op.t[0], hi = op.t[0];
     if (nt == 2) {
@@ -73,7 +74,7 @@ void fillUniformParts(TileOp& op) {
         hi = std::max(op.t[0], op.t[1]);
     }
     for (int u = 0; u < 16; u++) {
-        unsigned p = 256u * (unsigned)u;
+        unsigned p = th * (unsigned)u;
         if (nt >= 1) p = insertZero(p, lo);
         if (nt == 2) p = insertZero(p, hi);
         for (int s = 0; s < op.nsw; s++) {
@@ -90,7 +91,7 @@ void fillUniformParts(TileOp& op) {
 void laneSwaps(TileOp& op, int k) {
     op.nsw = 0;
     if (op.kind != (int)OpKind::Mat2 && op.kind != (int)OpKind::Mat4) {
-        fillUniformParts(op);
+        fillUniformParts(op, k);
         return;
     }
     const int nt = op.kind == (int)OpKind::Mat2 ? 1 : 2;
@@ -131,7 +132,7 @@ void laneSwaps(TileOp& op, int k) {
         if (r) bR.push_back(r);
         if (i < 4 && w) bW.push_back(w);
     }
-    fillUniformParts(op);
+    fillUniformParts(op, k);
 }
 
 namespace {

@@ -46,6 +46,11 @@ struct TileOp {
 // Also fills du / sdu, the wave-uniform parts of the work-item addresses.
 void laneSwaps(TileOp& op, int k);
 
+// Threads per workgroup of the GPU tile kernel for a tile of k bits: 256 up
+// to 2^11 fp64 / 2^12 fp32 amplitudes (32 KiB), 512 for the double tile, so
+// that every thread keeps 8 (fp64) / 16 (fp32) amplitudes.
+constexpr unsigned tileThreads(int k) { return k > (sizeof(real) == 8 ? 11 : 12) ? 512u : 256u; }
+
 // A phase of a pass: a run of ops executed with each thread holding 2^R
 // amplitudes in registers, namely the tile elements spanned by the R tile
 // bits reg[0..R-1] (reg slot r <-> tile bit reg[r]).  Ops whose targets are

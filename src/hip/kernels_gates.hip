@@ -190,9 +190,9 @@ __device__ __forceinline__ void applyLdsOp(T* sre, T* sim, unsigned n, const Til
 // per access instead of recomputing the insertion and the swizzle.
 // ---------------------------------------------------------------------------
 
-template <typename T, unsigned N>
+template <typename T, unsigned N, unsigned TH>
 __device__ __forceinline__ void mat2Tile(T* __restrict__ sre, T* __restrict__ sim, const TileOp& op) {
-    constexpr int P = N / 2 / 256;
+    constexpr int P = N / 2 / TH;
     static_assert(P <= 16, "TileOp::du holds 16 work-item groups");
     const int t = op.t[0];
     const unsigned cin = op.ctrlIn;
@@ -214,9 +214,9 @@ __device__ __forceinline__ void mat2Tile(T* __restrict__ sre, T* __restrict__ si
     }
 }
 
-template <typename T, unsigned N>
+template <typename T, unsigned N, unsigned TH>
 __device__ __forceinline__ void mat4Tile(T* __restrict__ sre, T* __restrict__ sim, const TileOp& op) {
-    constexpr int P = N / 4 / 256;
+    constexpr int P = N / 4 / TH;
     static_assert(P <= 16, "TileOp::du holds 16 work-item groups");
     const int a = op.t[0], b = op.t[1];
     const int lo = a < b ? a : b, hi = a < b ? b : a;
@@ -251,29 +251,29 @@ __device__ __forceinline__ void mat4Tile(T* __restrict__ sre, T* __restrict__ si
     }
 }
 
-template <typename T, unsigned N>
+template <typename T, unsigned N, unsigned TH>
 __device__ __forceinline__ void diagTile(T* __restrict__ sre, T* __restrict__ sim, const TileOp& op) {
-    constexpr int P = N / 256;
+    constexpr int P = N / TH;
     const unsigned cin = op.ctrlIn;
     const T tr = (T)op.m[0], ti = (T)op.m[1];
     const unsigned a0 = swz(threadIdx.x);
 #pragma unroll
     for (int u = 0; u < P; u++) {
-        const unsigned p = threadIdx.x + 256u * u;
+        const unsigned p = threadIdx.x + TH * u;
         if ((p & cin) != cin) continue;
-        const unsigned i = a0 ^ swz(256u * u);  // compile-time constant
+        const unsigned i = a0 ^ swz(TH * u);  // compile-time constant
         const T r = sre[i], im = sim[i];
         sre[i] = tr * r - ti * im;
         sim[i] = tr * im + ti * r;
     }
 }
 
-template <typename T, unsigned N>
+template <typename T, unsigned N, unsigned TH>
 __device__ __forceinline__ void applyTileOp(T* sre, T* sim, const TileOp& op) {
     switch ((OpKind)op.kind) {
-        case OpKind::Mat2: mat2Tile<T, N>(sre, sim, op); break;
-        case OpKind::Diag: diagTile<T, N>(sre, sim, op); break;
-        case OpKind::Mat4: mat4Tile<T, N>(sre, sim, op); break;
+        case OpKind::Mat2: mat2Tile<T, N, TH>(sre, sim, op); break;
+        case OpKind::Diag: diagTile<T, N, TH>(sre, sim, op); break;
+        case OpKind::Mat4: mat4Tile<T, N, TH>(sre, sim, op); break;
         case OpKind::DensChan2: applyDensChan2<T, true>(sre, sim, N, op); break;
     }
 }
@@ -570,16 +570,17 @@ __device__ __forceinline__ typename Vec16<T>::type ldsGetVec(const T* s, unsigne
 // vectors per array for the HBM <-> LDS moves.
 // MODE 0: ops one by one on LDS; 1: register phases; 2: dense blocks
 template <typename T, int K, int MODE>
-__global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void tilePassKernelK(T* __restrict__ re, T* __restrict__ im, TileArgs a,
+__global__ __launch_bounds__(tileThreads(K), (MODE == 1 || K > kTileQubits) ? 2 : 4) void tilePassKernelK(T* __restrict__ re, T* __restrict__ im, TileArgs a,
                                                        const TileOp* __restrict__ ops,
                                                        const TilePhase* __restrict__ phases,
                                                        const real* __restrict__ mats) {
-    constexpr int R = K - 8;  // 256 threads x 2^R = 2^K
+    constexpr unsigned TH = tileThreads(K);
+    constexpr int R = K - 8;  // 256 threads x 2^R = 2^K (register phases: TH = 256)
     constexpr bool PHASES = MODE != 0;
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::n;
     constexpr unsigned N = 1u << K;
-    constexpr int U = N / VN / 256;
+    constexpr int U = N / VN / TH;
     static_assert(U >= 1, "tile too small for the vector layout");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     T* sre = reinterpret_cast<T*>(smem);
@@ -587,7 +588,7 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
     long long* hiOff = reinterpret_cast<long long*>(sim + N);
     const int c = a.c;
     const int nh = 1 << (K - c);
-    for (int h = threadIdx.x; h < nh; h += 256) {
+    for (int h = threadIdx.x; h < nh; h += TH) {
         long long off = 0;
         for (int i = c; i < K; i++)
             if ((h >> (i - c)) & 1) off |= 1ll << a.pos[i];
@@ -599,7 +600,7 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
     long long off[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const unsigned p = (threadIdx.x + 256u * u) * VN;
+        const unsigned p = (threadIdx.x + TH * u) * VN;
         off[u] = (long long)(p & lowMask) + hiOff[p >> c];
     }
 
@@ -629,7 +630,7 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const unsigned p = (threadIdx.x + 256u * u) * VN;
+        const unsigned p = (threadIdx.x + TH * u) * VN;
         ldsPutVec<T>(sre, p, rr[u]);
         ldsPutVec<T>(sim, p, ri[u]);
     }
@@ -649,7 +650,7 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
                     for (int o = ph.opBegin; o < ph.opEnd; o++) {
                         const TileOp& op = ops[o];
                         if (((unsigned long long)base & op.ctrlOut) != op.ctrlOut) continue;
-                        applyTileOp<T, N>(sre, sim, op);
+                        applyTileOp<T, N, TH>(sre, sim, op);
                         __syncthreads();
                     }
                 } else if constexpr (MODE == 2) {
@@ -664,20 +665,20 @@ __global__ __launch_bounds__(256, (MODE == 1 || K > kTileQubits) ? 2 : 4) void t
             for (int o = 0; o < a.nOps; o++) {
                 const TileOp& op = ops[o];
                 if (((unsigned long long)base & op.ctrlOut) != op.ctrlOut) continue;
-                applyTileOp<T, N>(sre, sim, op);
+                applyTileOp<T, N, TH>(sre, sim, op);
                 __syncthreads();
             }
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const unsigned p = (threadIdx.x + 256u * u) * VN;
+            const unsigned p = (threadIdx.x + TH * u) * VN;
             streamStore(reinterpret_cast<V*>(re + base + off[u]), ldsGetVec<T>(sre, p));
             streamStore(reinterpret_cast<V*>(im + base + off[u]), ldsGetVec<T>(sim, p));
         }
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const unsigned p = (threadIdx.x + 256u * u) * VN;
+            const unsigned p = (threadIdx.x + TH * u) * VN;
             ldsPutVec<T>(sre, p, rr[u]);
             ldsPutVec<T>(sim, p, ri[u]);
         }
@@ -714,7 +715,8 @@ void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps, c
     } else if (a.k == kTileQubits + 1 && a.c >= vecBits && a.nPhases == 0) {
         // double tile (64 KiB of LDS): op by op, 2 resident workgroups per CU
         const long long g2 = a.numTiles < (long long)numCUs() * 2 ? a.numTiles : (long long)numCUs() * 2;
-        hipLaunchKernelGGL((tilePassKernelK<real, kTileQubits + 1, 0>), dim3((int)g2), dim3(256), lds, stream(), re,
+        hipLaunchKernelGGL((tilePassKernelK<real, kTileQubits + 1, 0>), dim3((int)g2),
+                           dim3(tileThreads(kTileQubits + 1)), lds, stream(), re,
                            im, a, dOps, dPhases, dMats);
     } else if (a.c >= vecBits) {
         hipLaunchKernelGGL((tilePassKernel<real, true>), dim3(grid), dim3(256), lds, stream(), re, im, a, dOps);
