@@ -88,6 +88,57 @@ void fillUniformParts(TileOp& op, int k) {
 }
 }  // namespace
 
+namespace {
+// swaps for (target mask, k): computed once per distinct pair
+struct SwapPlan {
+    int nsw = 0;
+    unsigned char a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+};
+
+SwapPlan computeSwaps(unsigned tmask, int k) {
+    SwapPlan plan;
+    int map[32], nf = 0;  // work-item bit i -> element bit map[i]
+    for (int bit = 0; bit < k; bit++)
+        if (!((tmask >> bit) & 1)) map[nf++] = bit;
+    // GF(2) bases in echelon form: slot[l] holds the vector with leading bit l
+    unsigned bR[8] = {0}, bW[8] = {0};
+    auto reduce = [](const unsigned* basis, unsigned v) {
+        for (int l = 7; l >= 0; l--)
+            if (((v >> l) & 1) && basis[l]) v ^= basis[l];
+        return v;
+    };
+    auto insert = [&](unsigned* basis, unsigned v) {
+        v = reduce(basis, v);
+        if (!v) return;
+        int l = 31 - __builtin_clz(v);
+        basis[l] = v;
+    };
+    for (int i = 0; i < 5 && i < nf; i++) {
+        auto fits = [&](int e) {
+            const unsigned v = ldsSwizzle(1u << e);
+            return reduce(bR, v & 31u) != 0 && (i >= 4 || reduce(bW, v & 15u) != 0);
+        };
+        if (!fits(map[i])) {
+            int j = -1;
+            for (int c = i + 1; c < nf; c++)
+                if (fits(map[c])) {
+                    j = c;
+                    break;
+                }
+            if (j < 0 || plan.nsw == 4) continue;  // best effort
+            plan.a[plan.nsw] = (unsigned char)map[i];
+            plan.b[plan.nsw] = (unsigned char)map[j];
+            plan.nsw++;
+            std::swap(map[i], map[j]);
+        }
+        const unsigned v = ldsSwizzle(1u << map[i]);
+        insert(bR, v & 31u);
+        if (i < 4) insert(bW, v & 15u);
+    }
+    return plan;
+}
+}  // namespace
+
 void laneSwaps(TileOp& op, int k) {
     op.nsw = 0;
     if (op.kind != (int)OpKind::Mat2 && op.kind != (int)OpKind::Mat4) {
@@ -97,40 +148,23 @@ void laneSwaps(TileOp& op, int k) {
     const int nt = op.kind == (int)OpKind::Mat2 ? 1 : 2;
     unsigned tmask = 0;
     for (int i = 0; i < nt; i++) tmask |= 1u << op.t[i];
-    int map[32], nf = 0;  // work-item bit i -> element bit map[i]
-    for (int b = 0; b < k; b++)
-        if (!((tmask >> b) & 1)) map[nf++] = b;
-    // GF(2) basis with distinct leading bits: reduce v against it (largest first)
-    auto reduce = [](const std::vector<unsigned>& basis, unsigned v) {
-        std::vector<unsigned> b = basis;
-        std::sort(b.rbegin(), b.rend());
-        for (unsigned x : b) v = std::min(v, v ^ x);
-        return v;
-    };
-    auto indep = [&](std::vector<unsigned>& basis, unsigned v) { return reduce(basis, v) != 0; };
-    std::vector<unsigned> bR, bW;
-    for (int i = 0; i < 5 && i < nf; i++) {
-        auto fits = [&](int e) {
-            const unsigned r = ldsSwizzle(1u << e) & 31u, w = ldsSwizzle(1u << e) & 15u;
-            return indep(bR, r) && (i >= 4 || indep(bW, w));
-        };
-        if (!fits(map[i])) {
-            int j = -1;
-            for (int c = i + 1; c < nf; c++)
-                if (fits(map[c])) {
-                    j = c;
-                    break;
-                }
-            if (j < 0 || op.nsw == 4) continue;  // best effort
-            op.swA[op.nsw] = (unsigned char)map[i];
-            op.swB[op.nsw] = (unsigned char)map[j];
-            op.nsw++;
-            std::swap(map[i], map[j]);
+    // memo: 1 + 2 targets among at most 16 tile bits, per tile size
+    static thread_local std::vector<std::pair<unsigned long long, SwapPlan>> memo;
+    const unsigned long long key = ((unsigned long long)k << 32) | tmask;
+    const SwapPlan* plan = nullptr;
+    for (auto& kv : memo)
+        if (kv.first == key) {
+            plan = &kv.second;
+            break;
         }
-        const unsigned v = ldsSwizzle(1u << map[i]);
-        const unsigned r = reduce(bR, v & 31u), w = reduce(bW, v & 15u);
-        if (r) bR.push_back(r);
-        if (i < 4 && w) bW.push_back(w);
+    if (!plan) {
+        memo.emplace_back(key, computeSwaps(tmask, k));
+        plan = &memo.back().second;
+    }
+    op.nsw = plan->nsw;
+    for (int s = 0; s < plan->nsw; s++) {
+        op.swA[s] = plan->a[s];
+        op.swB[s] = plan->b[s];
     }
     fillUniformParts(op, k);
 }

@@ -358,10 +358,12 @@ void flush(QuregImpl& q) {
     if (trace::on())
         trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
                      q.pending.size(), prog.passes.size());
-    // QUEST_CPU_PLANNER: 0 op by op, 1 register phases, 2 dense blocks (default)
+    // QUEST_CPU_PLANNER: 0 op by op (default, fastest on the host), 1 register
+    // phases, 2 dense blocks -- 1 and 2 emulate the GPU tile modes exactly
+    // (same plans, same per-thread decomposition) for testing them here
     static const int planner = [] {
         const char* e = getenv("QUEST_CPU_PLANNER");
-        return e ? atoi(e) : 2;
+        return e ? atoi(e) : 0;
     }();
     if (planner == 1)
         planPhases(prog, -1, regSlots());

@@ -85,3 +85,23 @@ def test_layered_circuit_pass_count(env, fuse_width):
     c.apply_oracle(o)
     assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
     reg.close()
+
+
+@pytest.mark.parametrize("planner", ["1", "2"])
+def test_gpu_tile_modes_emulated_on_host(planner):
+    """The host backend replays the GPU's register-phase (1) and dense-block
+    (2) plans with the same per-thread decomposition; run the fusion and
+    golden checks through them (subprocess: the mode is fixed per process)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QUEST_BACKEND="cpu", QUEST_CPU_PLANNER=planner)
+    out = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                          os.path.join(root, "tests", "test_fusion.py"), "-k", "not emulated"],
+                         cwd=root, env=env, capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
+    g = subprocess.run([sys.executable, "-m", "quest_amd.utils.golden"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=900)
+    assert g.returncode == 0 and " 0 failed" in g.stdout, g.stdout[-2000:]
