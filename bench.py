@@ -98,6 +98,18 @@ def main():
     stats = qa.capi.getQuESTStats()
 
     norm = reg.total_prob()  # sanity (outside the timed region)
+    # for reference, outside the timed region: one unfused gate (= one full
+    # streaming pass over the state), median of 5
+    qa.capi.setGateFusion(0)
+    singles = []
+    for _ in range(5):
+        reg.sync()
+        t1 = time.perf_counter()
+        reg.h(n // 2)
+        reg.sync()
+        singles.append(time.perf_counter() - t1)
+    qa.capi.setGateFusion(1)
+    unfused_gate_s = allreduce_max(sorted(singles)[2])
     s_per_gate = elapsed / max(gates, 1)
     result = {
         "metric": "single-qubit-gate time (s) vs #qubits, fp64 state-vector; 1/2/4/8-GPU scaling",
@@ -125,6 +137,7 @@ def main():
             "passes": stats["passes"],
             "swaps": stats["swaps"],
             "norm_error": abs(norm - 1.0),
+            "unfused_gate_s": unfused_gate_s,
             "backend": qa.capi.getQuESTBackend(),
         },
     }
