@@ -272,7 +272,7 @@ void runPhase(const TilePhase& ph, const TileProgram& prog, int k, i64 base, rea
 // OpenMP over tiles (each thread stages its own tile), as the reference's
 // CPU kernels parallelise their pair loops (QuEST_cpu.c, `#pragma omp
 // parallel for`); small registers stay on one thread.
-constexpr i64 kOmpMin = (i64)1 << 15;
+constexpr i64 kOmpMin = (i64)1 << 22;  // below ~4M amplitudes thread wake-up costs more than it saves
 
 void runProgram(QuregImpl& q, const TileProgram& prog) {
     for (const TilePass& ps : prog.passes) {
