@@ -28,10 +28,15 @@ int getGateFusion(void);
 /* Maximum number of qubits spanned by one fused pass (0 = default). */
 void setFusionMaxQubits(int numQubits);
 
-/* Backend tuning knobs (HIP build): "direct_kernels" (LDS-free kernel for a
- * pass holding one gate), "tile_mode" (0 op by op, 1 register phases, 2 dense blocks),
- * "tile_wg_per_cu".  Returns 1 if the key is known.  Also settable at start
- * via QUEST_DIRECT_KERNELS / QUEST_TILE_MODE / QUEST_TILE_WG_PER_CU. */
+/* Tuning knobs.  Any build: "fuse_blocks" (compose gate pairs into 4x4
+ * blocks before scheduling), "verify" (debug: re-run every fused flush op by
+ * op on a shadow copy of the state and exit with a report if the results
+ * differ; env QUEST_VERIFY=1, tolerance QUEST_VERIFY_TOL).  HIP build:
+ * "direct_kernels" (LDS-free kernel for a pass holding one gate), "tile_mode"
+ * (0 op by op, 1 register phases, 2 dense blocks), "tile_qubits",
+ * "tile_wg_per_cu", "direct_layout", "direct_low_to_tile".  Returns 1 if the
+ * key is known.  Also settable at start via QUEST_DIRECT_KERNELS /
+ * QUEST_TILE_MODE / QUEST_TILE_QUBITS / QUEST_TILE_WG_PER_CU / ... */
 int setQuESTTuning(const char* key, int value);
 
 /* Submit every queued operation of the register to the device (async). */
@@ -74,6 +79,7 @@ typedef struct QuESTStats {
     long long swaps;          /* global<->local qubit swaps (distributed) */
     long long bytesExchanged; /* bytes sent to other ranks */
     long long reductions;     /* reduction kernels */
+    long long verifiedFlushes; /* flushes checked op by op (QUEST_VERIFY=1 / tuning "verify") */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

@@ -79,7 +79,8 @@ class _Binding:
 
         class QuESTStats(C.Structure):
             _fields_ = [(n, C.c_longlong) for n in
-                        ("opsQueued", "passes", "fusedOps", "swaps", "bytesExchanged", "reductions")]
+                        ("opsQueued", "passes", "fusedOps", "swaps", "bytesExchanged", "reductions",
+                         "verifiedFlushes")]
 
         self.Complex, self.ComplexMatrix2, self.Vector = Complex, ComplexMatrix2, Vector
         self.ComplexArray, self.QASMLogger, self.Qureg = ComplexArray, QASMLogger, Qureg

@@ -167,6 +167,8 @@ int seedFromEnvOrTime(unsigned long key[2]) {
 void readEnvConfig() {
     if (const char* f = getenv("QUEST_FUSION")) rt().fusion = atoi(f) != 0;
     if (const char* k = getenv("QUEST_FUSE_QUBITS")) rt().fuseMaxQubits = atoi(k);
+    if (const char* v = getenv("QUEST_VERIFY")) rt().verify = atoi(v) != 0;
+    if (const char* t = getenv("QUEST_VERIFY_TOL")) rt().verifyTol = atof(t);
     if (const char* s = getenv("QUEST_EXCHANGE_SLICE_MB")) {
         long long mb = atoll(s);
         if (mb > 0) rt().exchangeSliceBytes = mb << 20;
@@ -898,6 +900,14 @@ int setQuESTTuning(const char* key, int value) {
         fuseBlocks() = value != 0;
         return 1;
     }
+    if (key && !strcmp(key, "verify")) {
+        rt().verify = value != 0;
+        return 1;
+    }
+    if (key && !strcmp(key, "verify_inject")) {  // fault injection for the verify test
+        rt().verifyInject = value != 0;
+        return 1;
+    }
     return be::setTuning(key, value) ? 1 : 0;
 }
 
@@ -953,6 +963,7 @@ void getQuESTStats(QuESTStats* s) {
     s->swaps = stats().swaps;
     s->bytesExchanged = stats().bytesExchanged;
     s->reductions = stats().reductions;
+    s->verifiedFlushes = stats().verifiedFlushes;
 }
 
 void resetQuESTStats(void) { stats() = Stats(); }

@@ -49,6 +49,8 @@ struct Rccl {
     ncclResult_t (*groupEnd)() = nullptr;
     const char* (*errorString)(ncclResult_t) = nullptr;
     ncclResult_t (*getVersion)(int*) = nullptr;
+    ncclResult_t (*getAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;  // optional
+    ncclResult_t (*commAbort)(ncclComm_t) = nullptr;                      // optional
 } R;
 
 int g_rank = 0, g_size = 1;
@@ -107,10 +109,51 @@ bool loadRccl() {
     sym(R.groupEnd, "ncclGroupEnd");
     sym(R.errorString, "ncclGetErrorString");
     sym(R.getVersion, "ncclGetVersion");
+    R.getAsyncError = reinterpret_cast<decltype(R.getAsyncError)>(dlsym(R.lib, "ncclCommGetAsyncError"));
+    R.commAbort = reinterpret_cast<decltype(R.commAbort)>(dlsym(R.lib, "ncclCommAbort"));
     return true;
 }
 
 hipStream_t S() { return hipk::stream(); }
+
+// Failure detection while the host waits on the stream (hipk::syncStream):
+// an asynchronous RCCL error (e.g. a peer's connection dropped) or no
+// progress for QUEST_COMM_TIMEOUT seconds (default 900; 0 = never) aborts the
+// communicator and ends this rank with a report, rather than leaving every
+// rank of the job blocked in a collective whose peer is gone.
+double commTimeout() {
+    static const double t = [] {
+        const char* e = getenv("QUEST_COMM_TIMEOUT");
+        return e ? atof(e) : 900.0;
+    }();
+    return t;
+}
+
+[[noreturn]] void abortComm(const char* why) {
+    fprintf(stderr, "QuEST: rank %d: %s; aborting the RCCL communicator\n", g_rank, why);
+    fflush(stderr);
+    if (R.commAbort && g_comm) R.commAbort(g_comm);
+    g_comm = nullptr;
+    exit(EXIT_FAILURE);
+}
+
+void watchdog(double elapsed) {
+    if (!g_comm) return;
+    if (R.getAsyncError) {
+        ncclResult_t r = ncclSuccess;
+        if (R.getAsyncError(g_comm, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress) {
+            char msg[256];
+            snprintf(msg, sizeof msg, "RCCL reported an asynchronous error: %s", R.errorString(r));
+            abortComm(msg);
+        }
+    }
+    if (commTimeout() > 0 && elapsed > commTimeout()) {
+        char msg[256];
+        snprintf(msg, sizeof msg, "no progress for %.0f s (QUEST_COMM_TIMEOUT) -- a peer rank may have failed",
+                 elapsed);
+        abortComm(msg);
+    }
+}
 
 // pinned host staging of at least `bytes` (socket transport)
 char* stage(size_t bytes) {
@@ -166,6 +209,7 @@ void init(int rank, int size) {
     }
     QA_HIP_CHECK(hipMalloc(&g_dScalars, sizeof(double) * 64));
     QA_HIP_CHECK(hipHostMalloc(&g_hScalars, sizeof(double) * 64, hipHostMallocDefault));
+    hipk::setSyncWatchdog(watchdog);
 }
 
 void finalize() {
@@ -177,7 +221,8 @@ void finalize() {
         g_socket = false;
     }
     if (g_comm) {
-        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        hipk::syncStream();
+        hipk::setSyncWatchdog(nullptr);
         R.commDestroy(g_comm);
         g_comm = nullptr;
         (void)hipFree(g_dScalars);
@@ -197,10 +242,10 @@ void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
     if (g_socket) {
         char* h = stage(2 * bytes);
         QA_HIP_CHECK(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, S()));
-        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        hipk::syncStream();
         sock::sendrecv(peer, h, h + bytes, bytes);
         QA_HIP_CHECK(hipMemcpyAsync(recv, h + bytes, bytes, hipMemcpyHostToDevice, S()));
-        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        hipk::syncStream();
         return;
     }
     QA_NCCL(R.groupStart(), "ncclGroupStart");
@@ -235,7 +280,7 @@ void allreduceSum(double* vals, int n) {
         QA_HIP_CHECK(hipMemcpyAsync(g_dScalars, g_hScalars, sizeof(double) * k, hipMemcpyHostToDevice, S()));
         QA_NCCL(R.allReduce(g_dScalars, g_dScalars, (size_t)k, ncclFloat64, ncclSum, g_comm, S()), "ncclAllReduce");
         QA_HIP_CHECK(hipMemcpyAsync(g_hScalars, g_dScalars, sizeof(double) * k, hipMemcpyDeviceToHost, S()));
-        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        hipk::syncStream();
         memcpy(vals + off, g_hScalars, sizeof(double) * k);
     }
 }
@@ -260,7 +305,7 @@ void bcastHost(void* buf, size_t bytes, int root) {
         QA_HIP_CHECK(hipMemcpyAsync(g_dScalars, g_hScalars, k, hipMemcpyHostToDevice, S()));
         QA_NCCL(R.broadcast(g_dScalars, g_dScalars, k, ncclUint8, root, g_comm, S()), "ncclBroadcast");
         QA_HIP_CHECK(hipMemcpyAsync(g_hScalars, g_dScalars, k, hipMemcpyDeviceToHost, S()));
-        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        hipk::syncStream();
         memcpy(p + off, g_hScalars, k);
     }
 }
@@ -274,10 +319,10 @@ void allgather(const void* send, void* recv, size_t bytesPerRank) {
         const size_t all = bytesPerRank * (size_t)g_size;
         char* h = stage(bytesPerRank + all);
         QA_HIP_CHECK(hipMemcpyAsync(h, send, bytesPerRank, hipMemcpyDeviceToHost, S()));
-        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        hipk::syncStream();
         sock::allgatherHost(h, h + bytesPerRank, bytesPerRank);
         QA_HIP_CHECK(hipMemcpyAsync(recv, h + bytesPerRank, all, hipMemcpyHostToDevice, S()));
-        QA_HIP_CHECK(hipStreamSynchronize(S()));
+        hipk::syncStream();
         return;
     }
     QA_NCCL(R.allGather(send, recv, bytesPerRank, ncclUint8, g_comm, S()), "ncclAllGather");

@@ -98,6 +98,11 @@ struct Runtime {
     bool fusion = true;        // QUEST_FUSION=0 disables gate fusion
     int fuseMaxQubits = 0;     // 0 = backend default
     i64 exchangeSliceBytes = 256ll << 20;  // QUEST_EXCHANGE_SLICE_MB
+    // QUEST_VERIFY=1: every fused flush is re-run op by op on a shadow copy
+    // of the state and compared (debug mode; doubles memory and time)
+    bool verify = false;
+    double verifyTol = 0;  // QUEST_VERIFY_TOL; 0 = 1e-10 (fp64) / 1e-4 (fp32)
+    bool verifyInject = false;  // test hook: corrupt the next verified flush once
 };
 Runtime& rt();
 

@@ -17,6 +17,21 @@ Stats& stats() {
     return s;
 }
 
+void verifyFlush(int qubits, size_t ops, size_t passes, double maxDiff) {
+    const double tol = rt().verifyTol > 0 ? rt().verifyTol : (sizeof(real) == 8 ? 1e-10 : 1e-4);
+    stats().verifiedFlushes++;
+    if (trace::on())
+        trace::event("verify", "\"qubits\": %d, \"ops\": %zu, \"passes\": %zu, \"max_diff\": %.3e", qubits, ops,
+                     passes, maxDiff);
+    if (maxDiff <= tol) return;
+    fprintf(stderr,
+            "QuEST verify: rank %d: a fused flush of %zu ops (%zu passes) on %d local qubits differs from op-by-op "
+            "execution by %.3e (tolerance %.1e)\n",
+            rt().rank, ops, passes, qubits, maxDiff, tol);
+    fflush(stderr);
+    exit(EXIT_FAILURE);
+}
+
 QuregImpl* impl(const Qureg& q) {
     QuregImpl* p = reinterpret_cast<QuregImpl*>(q.qasmLog);
     if (!p || p->magic != kQuregMagic) {

@@ -70,7 +70,13 @@ void readRange(QuregImpl& q, i64 start, real* re, real* im, i64 n);
 // runtime statistics (quest_amd.h: QuESTStats)
 struct Stats {
     long long opsQueued = 0, passes = 0, fusedOps = 0, swaps = 0, bytesExchanged = 0, reductions = 0;
+    long long verifiedFlushes = 0;
 };
 Stats& stats();
+
+// QUEST_VERIFY: compare the fused result of a flush with its op-by-op
+// re-execution; exits with a report when they differ by more than the
+// tolerance (src/core/router.cpp)
+void verifyFlush(int qubits, size_t ops, size_t passes, double maxDiff);
 
 }  // namespace qa

@@ -274,21 +274,21 @@ void runPhase(const TilePhase& ph, const TileProgram& prog, int k, i64 base, rea
 // parallel for`); small registers stay on one thread.
 constexpr i64 kOmpMin = (i64)1 << 22;  // below ~4M amplitudes thread wake-up costs more than it saves
 
-void runProgram(QuregImpl& q, const TileProgram& prog) {
+void runProgram(real* re, real* im, int L, const TileProgram& prog) {
     for (const TilePass& ps : prog.passes) {
         const unsigned n = 1u << ps.k;
         std::vector<i64> offs(n);
         for (unsigned p = 0; p < n; p++) offs[p] = tileOffset(ps, p);
-        const i64 tiles = (i64)1 << (q.L - ps.k);
-#pragma omp parallel if (q.numAmpsPerChunk >= kOmpMin)
+        const i64 tiles = (i64)1 << (L - ps.k);
+#pragma omp parallel if (((i64)1 << L) >= kOmpMin)
         {
             std::vector<real> br(n), bi(n);
 #pragma omp for schedule(static)
             for (i64 T = 0; T < tiles; T++) {
-                const i64 base = tileBase(ps, T, q.L);
+                const i64 base = tileBase(ps, T, L);
                 for (unsigned p = 0; p < n; p++) {
-                    br[p] = q.re[base + offs[p]];
-                    bi[p] = q.im[base + offs[p]];
+                    br[p] = re[base + offs[p]];
+                    bi[p] = im[base + offs[p]];
                 }
                 if (ps.phaseEnd > ps.phaseBegin) {
                     for (int h = ps.phaseBegin; h < ps.phaseEnd; h++)
@@ -301,8 +301,8 @@ void runProgram(QuregImpl& q, const TileProgram& prog) {
                     }
                 }
                 for (unsigned p = 0; p < n; p++) {
-                    q.re[base + offs[p]] = br[p];
-                    q.im[base + offs[p]] = bi[p];
+                    re[base + offs[p]] = br[p];
+                    im[base + offs[p]] = bi[p];
                 }
             }
         }
@@ -354,6 +354,8 @@ void flush(QuregImpl& q) {
     if (q.pending.empty()) return;
     const size_t opsIn = q.pending.size();
     TileProgram prog;
+    std::vector<Op> raw;
+    if (rt().verify) raw = q.pending;
     planTiles(q.pending, q.L, fuseQubits(), 4, rt().fusion, prog);
     if (trace::on())
         trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
@@ -370,7 +372,28 @@ void flush(QuregImpl& q) {
     else if (planner == 2)
         planDenseBlocks(prog, -1, regSlots());
     q.pending.clear();
-    runProgram(q, prog);
+    if (!rt().verify) {
+        runProgram(q.re, q.im, q.L, prog);
+        return;
+    }
+    // debug mode: the same ops one pass each, in order, on a shadow copy
+    std::vector<real> sr(q.re, q.re + q.numAmpsPerChunk), si(q.im, q.im + q.numAmpsPerChunk);
+    runProgram(q.re, q.im, q.L, prog);
+    const Stats keep = stats();
+    TileProgram ref;
+    planTiles(raw, q.L, fuseQubits(), 4, false, ref);
+    runProgram(sr.data(), si.data(), q.L, ref);
+    stats() = keep;
+    if (rt().verifyInject) {
+        rt().verifyInject = false;
+        q.re[0] += (real)0.5;
+    }
+    double diff = 0;
+    for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
+        const double d = std::hypot((double)q.re[i] - sr[i], (double)q.im[i] - si[i]);
+        diff = (d != d) ? INFINITY : std::max(diff, d);
+    }
+    verifyFlush(q.L, raw.size(), prog.passes.size(), diff);
 }
 
 void fill(QuregImpl& q, real re, real im) {

@@ -6,7 +6,10 @@
 // (src/comm/comm_rccl.cpp), so pack -> send/recv -> unpack needs no host
 // synchronisation.  The host blocks only when a value must come back
 // (reductions, amplitude reads) or at syncQuESTEnv.
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -37,7 +40,49 @@ char* g_progDev = nullptr;
 hipEvent_t g_slotEvent[kSlots];
 bool g_slotUsed[kSlots];
 int g_nextSlot = 0;
+
+void (*g_watchdog)(double) = nullptr;
+double syncTimeout() {
+    static const double t = [] {
+        const char* e = getenv("QUEST_SYNC_TIMEOUT");
+        return e ? atof(e) : 0.0;
+    }();
+    return t;
+}
 }  // namespace
+
+void setSyncWatchdog(void (*poll)(double)) { g_watchdog = poll; }
+
+void syncStream(hipEvent_t ev) {
+    if (!g_watchdog && syncTimeout() <= 0) {
+        if (ev)
+            QA_HIP_CHECK(hipEventSynchronize(ev));
+        else
+            syncStream();
+        return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    double nextPoll = 0.01;
+    for (long spin = 0;; spin++) {
+        const hipError_t e = ev ? hipEventQuery(ev) : hipStreamQuery(g_stream);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) fatal(ev ? "hipEventQuery" : "hipStreamQuery", hipGetErrorString(e), __FILE__, __LINE__);
+        (void)hipGetLastError();  // "not ready" is not an error; keep it out of the next launch check
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (syncTimeout() > 0 && el > syncTimeout()) {
+            fprintf(stderr,
+                    "QuEST: rank %d: device work has not finished after %.1f s (QUEST_SYNC_TIMEOUT); exiting\n",
+                    rt().rank, el);
+            fflush(stderr);
+            exit(EXIT_FAILURE);
+        }
+        if (g_watchdog && el >= nextPoll) {
+            g_watchdog(el);
+            nextPoll = el + 0.01;
+        }
+        if (spin > 2000) usleep(20);
+    }
+}
 
 Tuning& tuning() {
     static Tuning t = [] {
@@ -97,7 +142,7 @@ int contiguousLow(const TilePass& ps) {
 
 bool directEnabled() { return tuning().directKernels != 0; }
 
-void runProgram(QuregImpl& q, const std::vector<Op>& src, TileProgram& prog) {
+void runProgram(real* re, real* im, int L, const std::vector<Op>& src, TileProgram& prog, int tileMode) {
     // phase op ranges relative to their pass (the kernel sees the pass's ops)
     std::vector<TilePhase> rel = prog.phases;
     for (const TilePass& ps : prog.passes)
@@ -112,7 +157,7 @@ void runProgram(QuregImpl& q, const std::vector<Op>& src, TileProgram& prog) {
     if (total > kSlotBytes) fatal("tile program", "too many ops in one flush", __FILE__, __LINE__);
     const int s = g_nextSlot;
     g_nextSlot = (g_nextSlot + 1) % kSlots;
-    if (g_slotUsed[s]) QA_HIP_CHECK(hipEventSynchronize(g_slotEvent[s]));
+    if (g_slotUsed[s]) syncStream(g_slotEvent[s]);
     char* h = g_progHost + s * kSlotBytes;
     char* d = g_progDev + s * kSlotBytes;
     memcpy(h, prog.ops.data(), opBytes);
@@ -126,17 +171,17 @@ void runProgram(QuregImpl& q, const std::vector<Op>& src, TileProgram& prog) {
         const int nOps = ps.opEnd - ps.opBegin;
         stats().passes++;
         if (nOps > 1) stats().fusedOps += nOps;
-        if (nOps == 1 && directEnabled() && launchDirectOp(q.re, q.im, q.L, src[ps.opBegin])) continue;
+        if (nOps == 1 && directEnabled() && launchDirectOp(re, im, L, src[ps.opBegin])) continue;
         TileArgs a;
-        a.L = q.L;
+        a.L = L;
         a.k = ps.k;
         a.c = contiguousLow(ps);
         a.nOps = nOps;
         a.nPhases = ps.phaseEnd - ps.phaseBegin;
         a.pad = 0;
-        a.numTiles = 1ll << (q.L - ps.k);
+        a.numTiles = 1ll << (L - ps.k);
         for (int i = 0; i < 32; i++) a.pos[i] = i < ps.k ? ps.pos[i] : 0;
-        launchTilePass(q.re, q.im, a, dOps + ps.opBegin, dPh + ps.phaseBegin, dMats, tuning().tileMode);
+        launchTilePass(re, im, a, dOps + ps.opBegin, dPh + ps.phaseBegin, dMats, tileMode);
     }
     QA_HIP_CHECK(hipEventRecord(g_slotEvent[s], g_stream));
     g_slotUsed[s] = true;
@@ -167,7 +212,7 @@ void envInit(int rank, int numRanks, int localRank) {
 
 void envFinalize() {
     if (!g_stream) return;
-    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+    syncStream();
     for (int i = 0; i < kSlots; i++) (void)hipEventDestroy(g_slotEvent[i]);
     (void)hipHostFree(g_progHost);
     (void)hipFree(g_progDev);
@@ -177,7 +222,7 @@ void envFinalize() {
 }
 
 void deviceSync() {
-    if (g_stream) QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+    if (g_stream) syncStream();
 }
 
 std::string describe() {
@@ -247,7 +292,10 @@ void flush(QuregImpl& q) {
     trace::Range range("quest.flush");
     const size_t opsIn = q.pending.size();
     TileProgram prog;
-    planTiles(q.pending, q.L, tileQubits(q.L), sizeof(real) == 8 ? 4 : 5, rt().fusion, prog);
+    const int cmin = sizeof(real) == 8 ? 4 : 5;
+    std::vector<Op> raw;
+    if (rt().verify) raw = q.pending;
+    planTiles(q.pending, q.L, tileQubits(q.L), cmin, rt().fusion, prog);
     if (tuning().tileMode == 1)
         planPhases(prog, kTileQubits, kRegSlots);
     else if (tuning().tileMode == 2)
@@ -257,7 +305,32 @@ void flush(QuregImpl& q) {
                      q.pending.size(), prog.passes.size());
     std::vector<Op> src;
     src.swap(q.pending);
-    runProgram(q, src, prog);
+    if (!rt().verify) {
+        runProgram(q.re, q.im, q.L, src, prog, tuning().tileMode);
+        return;
+    }
+    // debug mode: the same ops one pass each (no fusion, no reordering, the
+    // direct kernels where they apply) on a shadow copy, then compare
+    const size_t bytes = sizeof(real) * (size_t)q.numAmpsPerChunk;
+    real *sr = nullptr, *si = nullptr;
+    QA_HIP_CHECK(hipMalloc(&sr, bytes));
+    QA_HIP_CHECK(hipMalloc(&si, bytes));
+    QA_HIP_CHECK(hipMemcpyAsync(sr, q.re, bytes, hipMemcpyDeviceToDevice, g_stream));
+    QA_HIP_CHECK(hipMemcpyAsync(si, q.im, bytes, hipMemcpyDeviceToDevice, g_stream));
+    runProgram(q.re, q.im, q.L, src, prog, tuning().tileMode);
+    const Stats keep = stats();
+    TileProgram ref;
+    planTiles(raw, q.L, tileQubits(q.L), cmin, false, ref);
+    runProgram(sr, si, q.L, raw, ref, 0);
+    stats() = keep;
+    if (rt().verifyInject) {
+        rt().verifyInject = false;
+        launchFill(q.re, q.im, 1, (real)0.5, (real)0);
+    }
+    const double diff = reduceMaxDiff(q.re, q.im, sr, si, q.numAmpsPerChunk);
+    QA_HIP_CHECK(hipFree(sr));
+    QA_HIP_CHECK(hipFree(si));
+    verifyFlush(q.L, raw.size(), prog.passes.size(), diff);
 }
 
 void fill(QuregImpl& q, real re, real im) {
@@ -284,14 +357,14 @@ void writeAmps(QuregImpl& q, i64 local, const real* re, const real* im, i64 n) {
     flush(q);
     QA_HIP_CHECK(hipMemcpyAsync(q.re + local, re, sizeof(real) * n, hipMemcpyHostToDevice, g_stream));
     QA_HIP_CHECK(hipMemcpyAsync(q.im + local, im, sizeof(real) * n, hipMemcpyHostToDevice, g_stream));
-    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+    syncStream();
 }
 
 void readAmps(QuregImpl& q, i64 local, real* re, real* im, i64 n) {
     flush(q);
     QA_HIP_CHECK(hipMemcpyAsync(re, q.re + local, sizeof(real) * n, hipMemcpyDeviceToHost, g_stream));
     QA_HIP_CHECK(hipMemcpyAsync(im, q.im + local, sizeof(real) * n, hipMemcpyDeviceToHost, g_stream));
-    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+    syncStream();
 }
 
 void copyState(QuregImpl& dst, QuregImpl& src) {
@@ -359,12 +432,12 @@ void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* br, const real* bi) 
 
 void bufferToHost(const real* buf, real* host, i64 n) {
     QA_HIP_CHECK(hipMemcpyAsync(host, buf, sizeof(real) * n, hipMemcpyDeviceToHost, g_stream));
-    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+    syncStream();
 }
 
 void hostToBuffer(const real* host, real* buf, i64 n) {
     QA_HIP_CHECK(hipMemcpyAsync(buf, host, sizeof(real) * n, hipMemcpyHostToDevice, g_stream));
-    QA_HIP_CHECK(hipStreamSynchronize(g_stream));
+    syncStream();
 }
 
 }  // namespace be

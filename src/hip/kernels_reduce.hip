@@ -180,6 +180,49 @@ __global__ __launch_bounds__(kThreads) void densFidelityKernel(const T* __restri
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// max over the block of a non-negative value; result valid in thread 0
+__device__ __forceinline__ double blockMax(double v) {
+    __shared__ double sh[kThreads / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0;
+    if (threadIdx.x < 64) {
+        r = (threadIdx.x < kThreads / 64) ? sh[threadIdx.x] : 0.0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) r = fmax(r, __shfl_xor(r, off, 64));
+    }
+    return r;
+}
+
+// max_i |a_i - b_i| over complex amplitudes (QUEST_VERIFY)
+template <typename T>
+__global__ __launch_bounds__(kThreads) void maxDiffKernel(const T* __restrict__ ar, const T* __restrict__ ai,
+                                                          const T* __restrict__ br, const T* __restrict__ bi,
+                                                          long long n, double* __restrict__ part) {
+    double m = 0;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double dr = (double)ar[i] - br[i], di = (double)ai[i] - bi[i];
+        // NaN anywhere must fail the check: fmax would drop it
+        const double d = sqrt(dr * dr + di * di);
+        m = (d != d) ? INFINITY : fmax(m, d);
+    }
+    const double s = blockMax(m);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void finishMaxKernel(const double* __restrict__ part, int nb,
+                                                            double* __restrict__ out) {
+    double m = 0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) m = fmax(m, part[i]);
+    const double s = blockMax(m);
+    if (threadIdx.x == 0) out[0] = s;
+}
+
 __global__ __launch_bounds__(kThreads) void finishKernel(const double* __restrict__ part, int nb, int nvals,
                                                          double* __restrict__ out) {
     for (int v = 0; v < nvals; v++) {
@@ -202,7 +245,7 @@ void finish(int nb, int nvals, double* result) {
     hipLaunchKernelGGL(finishKernel, dim3(1), dim3(kThreads), 0, stream(), g_partials, nb, nvals, g_out);
     QA_HIP_CHECK(hipGetLastError());
     QA_HIP_CHECK(hipMemcpyAsync(g_outHost, g_out, sizeof(double) * nvals, hipMemcpyDeviceToHost, stream()));
-    QA_HIP_CHECK(hipStreamSynchronize(stream()));
+    syncStream();
     for (int v = 0; v < nvals; v++) result[v] = g_outHost[v];
 }
 
@@ -236,6 +279,18 @@ void reduceInner(const real* ar, const real* ai, const real* br, const real* bi,
     hipLaunchKernelGGL(innerKernel<real>, dim3(nb), dim3(kThreads), 0, stream(), ar, ai, br, bi, n, g_partials);
     QA_HIP_CHECK(hipGetLastError());
     finish(nb, 2, out);
+}
+
+double reduceMaxDiff(const real* ar, const real* ai, const real* br, const real* bi, i64 n) {
+    ensureScratch();
+    const int nb = blocksFor(n);
+    hipLaunchKernelGGL(maxDiffKernel<real>, dim3(nb), dim3(kThreads), 0, stream(), ar, ai, br, bi, n, g_partials);
+    QA_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(finishMaxKernel, dim3(1), dim3(kThreads), 0, stream(), g_partials, nb, g_out);
+    QA_HIP_CHECK(hipGetLastError());
+    QA_HIP_CHECK(hipMemcpyAsync(g_outHost, g_out, sizeof(double), hipMemcpyDeviceToHost, stream()));
+    syncStream();
+    return g_outHost[0];
 }
 
 double reduceDensDiag(const real* re, i64 chunkAmps, const u64* offs, int nq, int skipBit, i64 chunkStart) {

@@ -23,6 +23,15 @@ namespace hipk {
 hipStream_t stream();   // the backend's compute stream (RCCL ops are ordered on it too)
 int numCUs();
 
+// Wait until `ev` (nullptr: everything queued on the stream) has completed.
+// With a watchdog -- installed by the RCCL transport, or QUEST_SYNC_TIMEOUT
+// seconds -- the wait polls instead of blocking, so a dead peer rank or a
+// kernel that never finishes ends the process with a report instead of a
+// silent hang.
+void syncStream(hipEvent_t ev = nullptr);
+// poll(elapsedSeconds) is called about every 10 ms while a wait is pending
+void setSyncWatchdog(void (*poll)(double elapsedSeconds));
+
 // runtime knobs (env QUEST_* at start-up, setQuESTTuning() afterwards)
 struct Tuning {
     int directKernels = 1;  // LDS-free kernels for single-op passes
@@ -127,6 +136,7 @@ void launchDensInitPure(real* re, real* im, i64 n, const real* pr, const real* p
 // reductions: results are written to `out` (device, doubles) and copied back
 double reduceSumSq(const real* re, const real* im, i64 n, int bit, int bitVal);
 void reduceInner(const real* ar, const real* ai, const real* br, const real* bi, i64 n, double out[2]);
+double reduceMaxDiff(const real* ar, const real* ai, const real* br, const real* bi, i64 n);
 double reduceDensDiag(const real* re, i64 chunkAmps, const u64* offs, int nq, int skipBit, i64 chunkStart);
 double reduceDensFidelity(const real* re, const real* im, i64 n, const real* pr, const real* pi, int nq,
                           i64 chunkStart);

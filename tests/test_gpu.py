@@ -370,3 +370,31 @@ def test_checkpoint_round_trip_gpu(genv, tmp_path):
     assert abs(s.inner(r) - 1) < 1e-12
     r.close()
     s.close()
+
+
+def test_sync_watchdog_reports_unfinished_work():
+    """QUEST_SYNC_TIMEOUT: a host wait on device work that takes longer than
+    the limit ends the process with a report (the same polling wait carries
+    the RCCL async-error / peer-timeout watchdog).  Subprocess: exits."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import quest_amd as qa\n"
+            "from quest_amd.ops import capi\n"
+            "env = qa.Env(); reg = qa.Register(env, 30)\n"
+            "capi.setGateFusion(0)\n"
+            "for _ in range(40):\n"
+            "    reg.h(20)\n"
+            "reg.sync()\n"
+            "print('FINISHED')\n")
+    envv = dict(os.environ, QUEST_BACKEND="hip", QUEST_SYNC_TIMEOUT="0.02")
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=envv, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode != 0 and "FINISHED" not in out.stdout, out.stdout
+    assert "QUEST_SYNC_TIMEOUT" in out.stderr, out.stderr[-2000:]
+    # and without the limit the same program completes
+    envv.pop("QUEST_SYNC_TIMEOUT")
+    ok = subprocess.run([sys.executable, "-c", code], cwd=root, env=envv, capture_output=True, text=True,
+                        timeout=300)
+    assert ok.returncode == 0 and "FINISHED" in ok.stdout, ok.stderr[-2000:]
