@@ -58,7 +58,7 @@ void syncStream(hipEvent_t ev) {
         if (ev)
             QA_HIP_CHECK(hipEventSynchronize(ev));
         else
-            syncStream();
+            QA_HIP_CHECK(hipStreamSynchronize(g_stream));
         return;
     }
     const auto t0 = std::chrono::steady_clock::now();
