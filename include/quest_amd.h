@@ -80,6 +80,9 @@ typedef struct QuESTStats {
     long long bytesExchanged; /* bytes sent to other ranks */
     long long reductions;     /* reduction kernels */
     long long verifiedFlushes; /* flushes checked op by op (QUEST_VERIFY=1 / tuning "verify") */
+    long long wavePasses;     /* passes run by the register-resident wave-tile engine */
+    long long waveOps;        /* ops of those passes, including transpositions */
+    long long waveTransposes; /* cross-lane transpositions among them */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

@@ -964,6 +964,9 @@ void getQuESTStats(QuESTStats* s) {
     s->bytesExchanged = stats().bytesExchanged;
     s->reductions = stats().reductions;
     s->verifiedFlushes = stats().verifiedFlushes;
+    s->wavePasses = stats().wavePasses;
+    s->waveOps = stats().waveOps;
+    s->waveTransposes = stats().waveTransposes;
 }
 
 void resetQuESTStats(void) { stats() = Stats(); }

@@ -71,6 +71,8 @@ void readRange(QuregImpl& q, i64 start, real* re, real* im, i64 n);
 struct Stats {
     long long opsQueued = 0, passes = 0, fusedOps = 0, swaps = 0, bytesExchanged = 0, reductions = 0;
     long long verifiedFlushes = 0;
+    long long wavePasses = 0;     // passes run by the wave-tile engine
+    long long waveOps = 0, waveTransposes = 0;  // their ops / cross-lane transpositions
 };
 Stats& stats();
 

@@ -264,6 +264,11 @@ bool& fuseBlocks() {
     return on;
 }
 
+int& fuseBlockQubits() {
+    static int q = 2;
+    return q;
+}
+
 void fuseGates(std::vector<Op>& ops) {
     const int n = (int)ops.size();
     if (n < 2) return;
@@ -274,7 +279,8 @@ void fuseGates(std::vector<Op>& ops) {
     for (int i = 0; i < n; i++) {
         const Op& op = ops[i];
         int q[2];
-        const int ns = support(op, q);
+        int ns = support(op, q);
+        if (ns > fuseBlockQubits()) ns = -1;
         if (ns < 0) {  // barrier on every qubit it touches
             for (int t = 0; t < op.nt; t++) last[op.t[t]] = -2;
             for (u64 c = op.ctrl; c; c &= c - 1) last[__builtin_ctzll(c)] = -2;

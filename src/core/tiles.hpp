@@ -118,6 +118,9 @@ void fuseGates(std::vector<Op>& ops);
 // Gate-block fusion in planTiles (env QUEST_FUSE_BLOCKS=0 / setQuESTTuning
 // "fuse_blocks" turn it off).
 bool& fuseBlocks();
+// Largest block fuseGates forms: 2 (4x4 blocks, default) or 1 (runs of
+// one-qubit gates only; the wave engine keeps CNOTs and controls apart)
+int& fuseBlockQubits();
 
 // Split `ops` (physical local positions, L local qubits) into passes of at
 // most kmax tile qubits (kmax >= cmin + 4).  With fuse=true ops are reordered

@@ -1,0 +1,241 @@
+#include "wave.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "router.hpp"
+
+namespace qa {
+
+namespace {
+
+constexpr int kInf = 1 << 30;
+
+// where[b]: < kWaveSlots: register slot; else lane bit (where - kWaveSlots)
+inline bool inSlot(int w) { return w < kWaveSlots; }
+inline int laneOf(int w) { return w - kWaveSlots; }
+
+// How a Mat2 is executed.  Diagonal matrices need no slot.
+enum class M2Class { Diag, Swap, Anti, Real, RealImag, General };
+
+M2Class classify(const real* m) {
+    // m: m00 re,im  m01 re,im  m10 re,im  m11 re,im
+    const bool offZero = m[2] == 0 && m[3] == 0 && m[4] == 0 && m[5] == 0;
+    const bool diagZero = m[0] == 0 && m[1] == 0 && m[6] == 0 && m[7] == 0;
+    if (offZero) return M2Class::Diag;
+    if (diagZero) {
+        if (m[2] == 1 && m[3] == 0 && m[4] == 1 && m[5] == 0) return M2Class::Swap;
+        return M2Class::Anti;
+    }
+    if (m[1] == 0 && m[3] == 0 && m[5] == 0 && m[7] == 0) return M2Class::Real;
+    if (m[1] == 0 && m[7] == 0 && m[2] == 0 && m[4] == 0) return M2Class::RealImag;
+    return M2Class::General;
+}
+
+struct Layout {
+    int where[kWaveBits];
+    int slotBit[kWaveSlots];
+    int laneBit[kWaveLanes];
+
+    void put(int b, int w) {
+        where[b] = w;
+        if (inSlot(w))
+            slotBit[w] = b;
+        else
+            laneBit[laneOf(w)] = b;
+    }
+};
+
+void masks(const Layout& lay, unsigned ctrlIn, unsigned& cReg, unsigned& cLane) {
+    cReg = cLane = 0;
+    for (int b = 0; b < kWaveBits; b++) {
+        if (!((ctrlIn >> b) & 1)) continue;
+        const int w = lay.where[b];
+        if (inSlot(w))
+            cReg |= 1u << w;
+        else
+            cLane |= 1u << laneOf(w);
+    }
+}
+
+WaveOp blank(int kind) {
+    WaveOp w;
+    memset(&w, 0, sizeof w);
+    w.kind = kind;
+    return w;
+}
+
+}  // namespace
+
+int waveTransposeCost(int laneBit) { return laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
+
+bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out) {
+    if (ps.k != kWaveBits) return false;
+    for (int i = 0; i < 4; i++)
+        if (ps.pos[i] != i) return false;
+    std::vector<M2Class> cls(nOps, M2Class::Diag);
+    for (int i = 0; i < nOps; i++) {
+        const OpKind k = (OpKind)ops[i].kind;
+        if (k == OpKind::Mat2)
+            cls[i] = classify(ops[i].m);
+        else if (k != OpKind::Diag)
+            return false;
+    }
+    // ops that need their target in a register slot
+    auto needsSlot = [&](int i) { return (OpKind)ops[i].kind == OpKind::Mat2 && cls[i] != M2Class::Diag; };
+    // next[i][b]: first op >= i needing tile bit b in a slot
+    std::vector<int> nextNeed((size_t)(nOps + 1) * kWaveBits, kInf);
+    for (int i = nOps - 1; i >= 0; i--) {
+        for (int b = 0; b < kWaveBits; b++) nextNeed[(size_t)i * kWaveBits + b] = nextNeed[(size_t)(i + 1) * kWaveBits + b];
+        if (needsSlot(i)) nextNeed[(size_t)i * kWaveBits + ops[i].t[0]] = i;
+    }
+    auto nextUse = [&](int i, int b) { return nextNeed[(size_t)i * kWaveBits + b]; };
+
+    WavePass wp;
+    for (int i = 0; i < kWaveBits; i++) wp.pos[i] = ps.pos[i];
+    // load layout: bit 0 -> slot 0, bits 1-3 -> lanes 0-2; of the higher tile
+    // bits those needed in a slot earliest take the other slots, the rest
+    // lanes 3-5
+    Layout lay;
+    lay.put(0, 0);
+    for (int l = 0; l < 3; l++) lay.put(l + 1, kWaveSlots + l);
+    std::vector<int> high;
+    for (int b = 4; b < kWaveBits; b++) high.push_back(b);
+    // bits above kWaveLanePosMax must take slots; then earliest need first
+    auto farPos = [&](int b) { return ps.pos[b] > kWaveLanePosMax; };
+    int nFar = 0;
+    for (int b : high) nFar += farPos(b);
+    if (nFar > kWaveSlots - 1) return false;
+    std::stable_sort(high.begin(), high.end(), [&](int x, int y) {
+        if (farPos(x) != farPos(y)) return farPos(x);
+        return nextUse(0, x) < nextUse(0, y);
+    });
+    for (int s = 1; s < kWaveSlots; s++) lay.put(high[s - 1], s);
+    for (int l = 3; l < kWaveLanes; l++) lay.put(high[kWaveSlots - 1 + l - 3], kWaveSlots + l);
+    for (int s = 0; s < kWaveSlots; s++) wp.ldSlot[s] = lay.slotBit[s];
+    for (int l = 0; l < kWaveLanes; l++) wp.ldLane[l] = lay.laneBit[l];
+
+    wp.opBegin = (int)out.ops.size();
+    auto transpose = [&](int s, int l) {
+        WaveOp w = blank((int)WKind::TR);
+        w.a = s;
+        w.b = l;
+        out.ops.push_back(w);
+        const int bs = lay.slotBit[s], bl = lay.laneBit[l];
+        lay.put(bs, kWaveSlots + l);
+        lay.put(bl, s);
+    };
+
+    for (int i = 0; i < nOps; i++) {
+        const TileOp& op = ops[i];
+        if ((OpKind)op.kind == OpKind::Diag) {
+            WaveOp w = blank((int)WKind::DIAG);
+            masks(lay, op.ctrlIn, w.cReg, w.cLane);
+            w.ctrlOut = op.ctrlOut;
+            w.m[0] = op.m[0];
+            w.m[1] = op.m[1];
+            out.ops.push_back(w);
+            continue;
+        }
+        const int t = op.t[0];
+        const real* m = op.m;
+        if (cls[i] == M2Class::Diag) {
+            WaveOp w;
+            if (m[0] == 1 && m[1] == 0) {  // phase on |1>: diagonal op on ctrl + target
+                w = blank((int)WKind::DIAG);
+                masks(lay, op.ctrlIn | (1u << t), w.cReg, w.cLane);
+                w.m[0] = m[6];
+                w.m[1] = m[7];
+            } else {
+                const int wt = lay.where[t];
+                w = blank(inSlot(wt) ? (int)WKind::D2S : (int)WKind::D2L);
+                w.a = inSlot(wt) ? wt : laneOf(wt);
+                masks(lay, op.ctrlIn, w.cReg, w.cLane);
+                w.m[0] = m[0];
+                w.m[1] = m[1];
+                w.m[2] = m[6];
+                w.m[3] = m[7];
+            }
+            w.ctrlOut = op.ctrlOut;
+            out.ops.push_back(w);
+            continue;
+        }
+        // target into a slot (slot 0 keeps tile bit 0 for the whole pass)
+        if (!inSlot(lay.where[t])) {
+            const int l = laneOf(lay.where[t]);
+            int victim = 1, far = -1;
+            for (int s = 1; s < kWaveSlots; s++) {
+                const int nu = nextUse(i, lay.slotBit[s]);
+                if (nu > far) {
+                    far = nu;
+                    victim = s;
+                }
+            }
+            transpose(victim, l);
+        }
+        WaveOp w;
+        switch (cls[i]) {
+            case M2Class::Swap: w = blank((int)WKind::SWAP); break;
+            case M2Class::Anti:
+                w = blank((int)WKind::ANTI);
+                w.m[0] = m[2];
+                w.m[1] = m[3];
+                w.m[2] = m[4];
+                w.m[3] = m[5];
+                break;
+            case M2Class::Real:
+                w = blank((int)WKind::M2R);
+                w.m[0] = m[0];
+                w.m[1] = m[2];
+                w.m[2] = m[4];
+                w.m[3] = m[6];
+                break;
+            case M2Class::RealImag:
+                w = blank((int)WKind::M2RI);
+                w.m[0] = m[0];
+                w.m[1] = m[3];
+                w.m[2] = m[5];
+                w.m[3] = m[6];
+                break;
+            default:
+                w = blank((int)WKind::M2);
+                for (int x = 0; x < 8; x++) w.m[x] = m[x];
+                break;
+        }
+        w.a = lay.where[t];
+        masks(lay, op.ctrlIn, w.cReg, w.cLane);
+        w.ctrlOut = op.ctrlOut;
+        out.ops.push_back(w);
+    }
+    // store layout: tile bits 1-3 back on lane bits 0-2 (bit 0 never left slot 0)
+    for (int l = 0; l < 3; l++) {
+        const int b = l + 1;
+        const int w = lay.where[b];
+        if (w == kWaveSlots + l) continue;
+        if (inSlot(w)) {
+            transpose(w, l);
+        } else {
+            // b sits on another lane bit (>= 3): through slot 1
+            transpose(1, laneOf(w));
+            transpose(1, l);
+        }
+    }
+    // lane bits 3.. may not carry positions above kWaveLanePosMax at store
+    for (int l = 3; l < kWaveLanes; l++) {
+        if (!farPos(lay.laneBit[l])) continue;
+        int s = -1;
+        for (int x = 1; x < kWaveSlots && s < 0; x++)
+            if (!farPos(lay.slotBit[x])) s = x;
+        if (s < 0) return false;  // cannot happen: at most kWaveSlots - 1 far bits
+        transpose(s, l);
+    }
+    for (int s = 0; s < kWaveSlots; s++) wp.stSlot[s] = lay.slotBit[s];
+    for (int l = 0; l < kWaveLanes; l++) wp.stLane[l] = lay.laneBit[l];
+    wp.opEnd = (int)out.ops.size();
+    out.passes.push_back(wp);
+    stats().waveOps += wp.opEnd - wp.opBegin;
+    for (int o = wp.opBegin; o < wp.opEnd; o++) stats().waveTransposes += out.ops[o].kind == (int)WKind::TR;
+    return true;
+}
+
+}  // namespace qa

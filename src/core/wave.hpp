@@ -1,0 +1,92 @@
+// Wave-tile programs: the register-resident pass engine of the HIP backend
+// (fp64), planned on the host.
+//
+// A pass of the ordinary tile planner (tiles.hpp) with exactly kWaveBits tile
+// bits is executed by ONE wave per tile: each of the 64 lanes holds 16
+// amplitudes in registers, so the wave holds the whole 2^10-amplitude tile
+// and no LDS and no barrier is involved.  A tile bit lives either in a
+// register *slot* (bit s of the register index j, s < 5) or in a *lane bit*
+// (bit l of the lane id, l < 6):
+//
+//   * gates whose target is in a slot run in registers (pairs j, j | 2^s);
+//   * diagonal gates and every control work wherever their bits are
+//     (per-register uniform predicates / per-lane predicates);
+//   * a target held by a lane bit is first exchanged with a slot by a
+//     cross-lane transposition (TR): DPP row shifts / quad permutes for lane
+//     bits 0-3, v_permlane16/32_swap for lane bits 4-5 -- VALU work only.
+//
+// Loads and stores need tile bit 0 in slot 0 (the two halves of a 16-byte
+// vector) and tile bits 1-3 in lane bits 0-2 (eight lanes cover one 128-byte
+// line); the other 7 tile bits can sit in any of slots 1-4 / lane bits 3-5,
+// chosen per pass for loads and whatever the ops left for stores.
+//
+// Gates are lowered to structure-specific kinds (real, real-diagonal /
+// imaginary-off-diagonal, anti-diagonal, Pauli-X swap, diagonal), so e.g. a
+// Hadamard costs 4 fp64 operations per amplitude instead of 8 and an X or a
+// CNOT none -- the fused LDS kernel was bound by fp64 FMA issue and LDS.
+#pragma once
+
+#include <vector>
+
+#include "tiles.hpp"
+
+namespace qa {
+
+#ifndef QA_WAVE_SLOTS
+#define QA_WAVE_SLOTS 4
+#endif
+// 2^4 amplitudes per lane: with 2^5 the compiler could not keep the
+// loop-carried tile in registers (spills at any occupancy)
+constexpr int kWaveSlots = QA_WAVE_SLOTS;
+constexpr int kWaveLanes = 6;   // 64 lanes
+constexpr int kWaveBits = kWaveSlots + kWaveLanes;
+constexpr int kWaveLanePosMax = 27;
+
+enum class WKind : int {
+    M2 = 0,    // general 2x2 on slot a
+    M2R = 1,   // real 2x2 on slot a (m[0..3] = m00 m01 m10 m11)
+    M2RI = 2,  // real diagonal / imaginary off-diagonal on slot a (m = m00 Im(m01) Im(m10) m11)
+    ANTI = 3,  // anti-diagonal on slot a (m = m01 re,im, m10 re,im)
+    SWAP = 4,  // Pauli X on slot a (controls make it CNOT / Toffoli)
+    DIAG = 5,  // multiply every element whose (cReg, cLane) bits are 1 by m[0] + i m[1]
+    D2S = 6,   // diagonal 2x2 on the bit of slot a (m = d0 re,im, d1 re,im)
+    D2L = 7,   // diagonal 2x2 on lane bit a
+    TR = 8,    // transpose slot a with lane bit b (never masked)
+};
+
+// One op, uploaded as-is (uniform: read through the scalar cache).
+struct WaveOp {
+    int kind;
+    int a, b;
+    unsigned cReg;    // register slots that must be 1
+    unsigned cLane;   // lane bits that must be 1
+    int pad;
+    u64 ctrlOut;      // physical bits outside the tile that must be 1
+    real m[8];
+};
+
+struct WavePass {
+    int pos[kWaveBits];        // tile bit -> physical position (pos[i] = i for i < 4)
+    int opBegin = 0, opEnd = 0;
+    int ldSlot[kWaveSlots];    // tile bit held by slot s at load
+    int ldLane[kWaveLanes];    // tile bit held by lane bit l at load
+    int stSlot[kWaveSlots];    // ... at store
+    int stLane[kWaveLanes];
+};
+
+struct WaveProgram {
+    std::vector<WavePass> passes;
+    std::vector<WaveOp> ops;
+};
+
+// Lower one tile pass (its ops in tile-local coordinates) to a wave pass.
+// False if the pass cannot run on the wave engine (tile size other than
+// kWaveBits, non-contiguous low bits, Mat4 / DensChan2 ops, too many tile
+// bits above kWaveLanePosMax).
+bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out);
+
+// Cost in VALU instructions per lane of one transposition with lane bit l
+// (for the planner's statistics and tests).
+int waveTransposeCost(int laneBit);
+
+}  // namespace qa

@@ -14,6 +14,7 @@
 #include "../core/backend.hpp"
 #include "../core/router.hpp"
 #include "../core/tiles.hpp"
+#include "../core/wave.hpp"
 #include "../core/trace.hpp"
 
 namespace qa {
@@ -274,37 +275,174 @@ void runPhase(const TilePhase& ph, const TileProgram& prog, int k, i64 base, rea
 // parallel for`); small registers stay on one thread.
 constexpr i64 kOmpMin = (i64)1 << 22;  // below ~4M amplitudes thread wake-up costs more than it saves
 
-void runProgram(real* re, real* im, int L, const TileProgram& prog) {
-    for (const TilePass& ps : prog.passes) {
-        const unsigned n = 1u << ps.k;
-        std::vector<i64> offs(n);
-        for (unsigned p = 0; p < n; p++) offs[p] = tileOffset(ps, p);
-        const i64 tiles = (i64)1 << (L - ps.k);
+void runTilePass(real* re, real* im, int L, const TileProgram& prog, const TilePass& ps) {
+    const unsigned n = 1u << ps.k;
+    std::vector<i64> offs(n);
+    for (unsigned p = 0; p < n; p++) offs[p] = tileOffset(ps, p);
+    const i64 tiles = (i64)1 << (L - ps.k);
 #pragma omp parallel if (((i64)1 << L) >= kOmpMin)
-        {
-            std::vector<real> br(n), bi(n);
+    {
+        std::vector<real> br(n), bi(n);
 #pragma omp for schedule(static)
-            for (i64 T = 0; T < tiles; T++) {
-                const i64 base = tileBase(ps, T, L);
-                for (unsigned p = 0; p < n; p++) {
-                    br[p] = re[base + offs[p]];
-                    bi[p] = im[base + offs[p]];
-                }
-                if (ps.phaseEnd > ps.phaseBegin) {
-                    for (int h = ps.phaseBegin; h < ps.phaseEnd; h++)
-                        runPhase(prog.phases[h], prog, ps.k, base, br.data(), bi.data());
-                } else {
-                    for (int o = ps.opBegin; o < ps.opEnd; o++) {
-                        const TileOp& op = prog.ops[o];
-                        if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
-                        applyTileOp(op, ps.k, br.data(), bi.data());
-                    }
-                }
-                for (unsigned p = 0; p < n; p++) {
-                    re[base + offs[p]] = br[p];
-                    im[base + offs[p]] = bi[p];
+        for (i64 T = 0; T < tiles; T++) {
+            const i64 base = tileBase(ps, T, L);
+            for (unsigned p = 0; p < n; p++) {
+                br[p] = re[base + offs[p]];
+                bi[p] = im[base + offs[p]];
+            }
+            if (ps.phaseEnd > ps.phaseBegin) {
+                for (int h = ps.phaseBegin; h < ps.phaseEnd; h++)
+                    runPhase(prog.phases[h], prog, ps.k, base, br.data(), bi.data());
+            } else {
+                for (int o = ps.opBegin; o < ps.opEnd; o++) {
+                    const TileOp& op = prog.ops[o];
+                    if (((u64)base & op.ctrlOut) != op.ctrlOut) continue;
+                    applyTileOp(op, ps.k, br.data(), bi.data());
                 }
             }
+            for (unsigned p = 0; p < n; p++) {
+                re[base + offs[p]] = br[p];
+                im[base + offs[p]] = bi[p];
+            }
+        }
+    }
+}
+
+// Wave-tile emulation: 64 "lanes" x 32 register slots per tile, exactly the
+// data movement of the GPU wave kernel (src/hip/kernels_wave.hip), so the
+// planner's transpositions and layouts are validated on CPU.
+constexpr int kWaveRegs = 1 << kWaveSlots;
+
+void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) {
+    const WKind kind = (WKind)w.kind;
+    if (kind == WKind::TR) {
+        const int s = w.a, l = w.b;
+        for (int j = 0; j < kWaveRegs; j++) {
+            if ((j >> s) & 1) continue;
+            const int f = j | (1 << s);
+            for (int L0 = 0; L0 < 64; L0++) {
+                if ((L0 >> l) & 1) continue;
+                const int L1 = L0 | (1 << l);
+                std::swap(vr[L1][j], vr[L0][f]);
+                std::swap(vi[L1][j], vi[L0][f]);
+            }
+        }
+        return;
+    }
+    const real* m = w.m;
+    for (int lane = 0; lane < 64; lane++) {
+        if (((unsigned)lane & w.cLane) != w.cLane) continue;
+        real* r = vr[lane];
+        real* i = vi[lane];
+        if (kind == WKind::DIAG || kind == WKind::D2S || kind == WKind::D2L) {
+            for (int j = 0; j < kWaveRegs; j++) {
+                if (((unsigned)j & w.cReg) != w.cReg) continue;
+                real tr = m[0], ti = m[1];
+                if (kind == WKind::D2S && ((j >> w.a) & 1)) tr = m[2], ti = m[3];
+                if (kind == WKind::D2L && ((lane >> w.a) & 1)) tr = m[2], ti = m[3];
+                const real x = r[j], y = i[j];
+                r[j] = tr * x - ti * y;
+                i[j] = tr * y + ti * x;
+            }
+            continue;
+        }
+        const int a = w.a;
+        for (int j = 0; j < kWaveRegs; j++) {
+            if ((j >> a) & 1) continue;
+            if (((unsigned)j & w.cReg) != w.cReg) continue;
+            const int f = j | (1 << a);
+            const real r0 = r[j], i0 = i[j], r1 = r[f], i1 = i[f];
+            switch (kind) {
+                case WKind::M2:
+                    r[j] = m[0] * r0 - m[1] * i0 + m[2] * r1 - m[3] * i1;
+                    i[j] = m[0] * i0 + m[1] * r0 + m[2] * i1 + m[3] * r1;
+                    r[f] = m[4] * r0 - m[5] * i0 + m[6] * r1 - m[7] * i1;
+                    i[f] = m[4] * i0 + m[5] * r0 + m[6] * i1 + m[7] * r1;
+                    break;
+                case WKind::M2R:
+                    r[j] = m[0] * r0 + m[1] * r1;
+                    i[j] = m[0] * i0 + m[1] * i1;
+                    r[f] = m[2] * r0 + m[3] * r1;
+                    i[f] = m[2] * i0 + m[3] * i1;
+                    break;
+                case WKind::M2RI:
+                    r[j] = m[0] * r0 - m[1] * i1;
+                    i[j] = m[0] * i0 + m[1] * r1;
+                    r[f] = m[3] * r1 - m[2] * i0;
+                    i[f] = m[3] * i1 + m[2] * r0;
+                    break;
+                case WKind::ANTI:
+                    r[j] = m[0] * r1 - m[1] * i1;
+                    i[j] = m[0] * i1 + m[1] * r1;
+                    r[f] = m[2] * r0 - m[3] * i0;
+                    i[f] = m[2] * i0 + m[3] * r0;
+                    break;
+                case WKind::SWAP:
+                    r[j] = r1;
+                    i[j] = i1;
+                    r[f] = r0;
+                    i[f] = i0;
+                    break;
+                default: break;
+            }
+        }
+    }
+}
+
+void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {
+    static thread_local i64 ld[64][kWaveRegs], st[64][kWaveRegs];
+    auto offsetOf = [&](const int* slotBit, const int* laneBit, int lane, int j) {
+        i64 off = 0;
+        for (int s = 0; s < kWaveSlots; s++)
+            if ((j >> s) & 1) off |= (i64)1 << ps.pos[slotBit[s]];
+        for (int l = 0; l < kWaveLanes; l++)
+            if ((lane >> l) & 1) off |= (i64)1 << ps.pos[laneBit[l]];
+        return off;
+    };
+    for (int lane = 0; lane < 64; lane++)
+        for (int j = 0; j < kWaveRegs; j++) {
+            ld[lane][j] = offsetOf(ps.ldSlot, ps.ldLane, lane, j);
+            st[lane][j] = offsetOf(ps.stSlot, ps.stLane, lane, j);
+        }
+    TilePass tp;
+    tp.k = kWaveBits;
+    for (int b = 0; b < kWaveBits; b++) tp.pos[b] = ps.pos[b];
+    const i64 tiles = (i64)1 << (L - kWaveBits);
+#pragma omp parallel if (((i64)1 << L) >= kOmpMin)
+    {
+        std::vector<real> bufR(64 * kWaveRegs), bufI(64 * kWaveRegs);
+        real(*vr)[kWaveRegs] = reinterpret_cast<real(*)[kWaveRegs]>(bufR.data());
+        real(*vi)[kWaveRegs] = reinterpret_cast<real(*)[kWaveRegs]>(bufI.data());
+#pragma omp for schedule(static)
+        for (i64 T = 0; T < tiles; T++) {
+            const i64 base = tileBase(tp, T, L);
+            for (int lane = 0; lane < 64; lane++)
+                for (int j = 0; j < kWaveRegs; j++) {
+                    vr[lane][j] = re[base + ld[lane][j]];
+                    vi[lane][j] = im[base + ld[lane][j]];
+                }
+            for (int o = ps.opBegin; o < ps.opEnd; o++) {
+                const WaveOp& w = wp.ops[o];
+                if (((u64)base & w.ctrlOut) != w.ctrlOut) continue;
+                applyWaveOp(w, vr, vi);
+            }
+            for (int lane = 0; lane < 64; lane++)
+                for (int j = 0; j < kWaveRegs; j++) {
+                    re[base + st[lane][j]] = vr[lane][j];
+                    im[base + st[lane][j]] = vi[lane][j];
+                }
+        }
+    }
+}
+
+void runProgram(real* re, real* im, int L, const TileProgram& prog, bool wave = false) {
+    for (const TilePass& ps : prog.passes) {
+        WaveProgram wp;
+        if (wave && planWavePass(ps, prog.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, wp)) {
+            runWavePass(re, im, L, wp, wp.passes[0]);
+            stats().wavePasses++;
+        } else {
+            runTilePass(re, im, L, prog, ps);
         }
         stats().passes++;
         if (ps.opEnd - ps.opBegin > 1) stats().fusedOps += ps.opEnd - ps.opBegin;
@@ -356,29 +494,32 @@ void flush(QuregImpl& q) {
     TileProgram prog;
     std::vector<Op> raw;
     if (rt().verify) raw = q.pending;
-    planTiles(q.pending, q.L, fuseQubits(), 4, rt().fusion, prog);
-    if (trace::on())
-        trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
-                     q.pending.size(), prog.passes.size());
     // QUEST_CPU_PLANNER: 0 op by op (default, fastest on the host), 1 register
-    // phases, 2 dense blocks -- 1 and 2 emulate the GPU tile modes exactly
-    // (same plans, same per-thread decomposition) for testing them here
+    // phases, 2 dense blocks, 3 wave tiles -- 1..3 emulate the GPU tile modes
+    // exactly (same plans, same per-thread / per-lane decomposition) for
+    // testing them here
     static const int planner = [] {
         const char* e = getenv("QUEST_CPU_PLANNER");
         return e ? atoi(e) : 0;
     }();
+    const bool wave = planner == 3 && q.L >= kWaveBits;
+    fuseBlockQubits() = wave ? 1 : 2;
+    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), 4, rt().fusion, prog);
+    if (trace::on())
+        trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
+                     q.pending.size(), prog.passes.size());
     if (planner == 1)
         planPhases(prog, -1, regSlots());
     else if (planner == 2)
         planDenseBlocks(prog, -1, regSlots());
     q.pending.clear();
     if (!rt().verify) {
-        runProgram(q.re, q.im, q.L, prog);
+        runProgram(q.re, q.im, q.L, prog, wave);
         return;
     }
     // debug mode: the same ops one pass each, in order, on a shadow copy
     std::vector<real> sr(q.re, q.re + q.numAmpsPerChunk), si(q.im, q.im + q.numAmpsPerChunk);
-    runProgram(q.re, q.im, q.L, prog);
+    runProgram(q.re, q.im, q.L, prog, wave);
     const Stats keep = stats();
     TileProgram ref;
     planTiles(raw, q.L, fuseQubits(), 4, false, ref);

@@ -1,0 +1,584 @@
+#!/usr/bin/env python3
+"""Generator of the wave-tile pass kernel in gfx950 assembly (fp64).
+
+Why assembly: the kernel keeps a 2^(R+6)-amplitude tile in VGPRs across a
+runtime-dispatched list of ops.  Written in HIP C++, LLVM's structurizer and
+register allocator turned every dispatch arm into copies of the whole tile
+(hundreds of v_mov per op, spills at any occupancy).  Here the tile lives in
+FIXED registers for the whole kernel and every op handler updates it in
+place; the host plan (src/core/wave.hpp) picks the handler of each op, whose
+byte offset from the dispatch anchor is stored in the op record, and the
+kernel jumps there with s_setpc_b64.
+
+    python tools/gen_wave_asm.py asm   --slots 4 --out build/wave/wave_kernel.s
+    python tools/gen_wave_asm.py embed --obj build/wave/wave_kernel.o \
+        --hsaco build/wave/wave_kernel.hsaco --out build/wave/wave_image.inc
+
+Register plan (R = slots, NS = 2^R amplitudes per lane):
+    v[2j : 2j+1]              re of register j        (j < NS)
+    v[2NS+2j : 2NS+2j+1]      im of register j
+    T0..T3 (4 doubles)        temporaries;  C0, C1 per-lane coefficients
+    vLane / vLdB / vStB       lane id, per-lane load / store byte offsets
+Device records (host side: src/hip/backend_hip.hip, WaveLaunchDev / WaveOpDev):
+    launch + 0    u64 numTiles          + 8   u64 waveStride
+           + 16   u32 nOps              + 24  u32 pos[16]
+           + 88   u64 ldGroupByte[16]   + 216 u64 stGroupByte[16]
+           + 344  u32 ldLaneByte[64]    + 600 u32 stLaneByte[64]
+           + 1024 WaveOpDev ops[]  (96 B: i32 handler, u32 cReg, u32 cLane,
+                  u32 aux, u64 ctrlOut, u64 pad, f64 m[8])
+Semantics of every op: src/core/wave.hpp (and the CPU emulation in
+src/cpu/backend_cpu.cpp applyWaveOp, which the tests compare against).
+"""
+import argparse
+import struct
+import sys
+
+KINDS = ["M2", "M2R", "M2RI", "ANTI", "SWAP"]
+# handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
+def idx_slot(kind, s, ctrl):
+    return KINDS.index(kind) * 16 + s * 2 + ctrl          # 0..79
+
+
+def idx_d2s(s, ctrl):
+    return 80 + s * 2 + ctrl                               # 80..95
+
+
+def idx_d2l(ctrl):
+    return 96 + ctrl
+
+
+IDX_DIAG = 98
+
+
+def idx_tr(s, l):
+    return 100 + s * 6 + l                                 # 100..135
+
+
+TABLE = 136
+
+
+class Gen:
+    def __init__(self, R):
+        self.R = R
+        self.NS = 1 << R
+        self.lines = []
+        D = 4 * self.NS
+        self.D = D
+        self.T = [D + 0, D + 2, D + 4, D + 6]   # temporaries (double pairs)
+        self.C0, self.C1 = D + 8, D + 10
+        self.vLane, self.vLdB, self.vStB, self.vTmp = D + 12, D + 13, D + 14, D + 15
+        self.nvgpr = D + 16
+        self.handlers = {}
+
+    # ---- helpers --------------------------------------------------------
+    def e(self, s):
+        self.lines.append("\t" + s)
+
+    def label(self, name):
+        self.lines.append(name + ":")
+
+    def re(self, j):
+        return 2 * j
+
+    def im(self, j):
+        return 2 * self.NS + 2 * j
+
+    @staticmethod
+    def vp(r):
+        return f"v[{r}:{r + 1}]"
+
+    @staticmethod
+    def sm(k):  # coefficient m[k] (double) in SGPRs
+        return f"s[{76 + 2 * k}:{77 + 2 * k}]"
+
+    def handler(self, idx, name):
+        lab = f"wh_{name}"
+        self.handlers[idx] = lab
+        self.lines.append("")
+        self.lines.append(f"\t.p2align 2")
+        self.label(lab)
+
+    def back(self):
+        self.e("s_branch .Lop_loop")
+
+    # ---- predication: per register j, exec = lanes whose controls hold ----
+    def ctrl_begin(self):
+        # LM (s[96:97]) = lanes with (lane & cLane) == cLane
+        self.e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
+        self.e(f"v_cmp_eq_u32_e64 s[96:97], s70, v{self.vTmp}")
+        self.e("s_nop 4")
+
+    def ctrl_j(self, j, skip):
+        # exec = (j & cReg) == cReg ? LM : 0
+        self.e(f"s_and_b32 s98, s69, {j}")
+        self.e("s_cmp_eq_u32 s98, s69")
+        self.e("s_cselect_b64 s[98:99], s[96:97], 0")
+        self.e("s_mov_b64 exec, s[98:99]")
+        self.e(f"s_cbranch_execz {skip}")
+
+    def ctrl_end(self):
+        self.e("s_mov_b64 exec, -1")
+
+    # ---- pair math (in place, registers of j and f) ---------------------
+    def pair(self, kind, j, f):
+        r0, i0, r1, i1 = self.vp(self.re(j)), self.vp(self.im(j)), self.vp(self.re(f)), self.vp(self.im(f))
+        T = [self.vp(t) for t in self.T]
+        m = self.sm
+        e = self.e
+        if kind == "M2":
+            e(f"v_mul_f64 {T[0]}, {m(0)}, {r0}")
+            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i0}, {T[0]}")
+            e(f"v_fma_f64 {T[0]}, {m(2)}, {r1}, {T[0]}")
+            e(f"v_fma_f64 {T[0]}, -{m(3)}, {i1}, {T[0]}")
+            e(f"v_mul_f64 {T[1]}, {m(0)}, {i0}")
+            e(f"v_fma_f64 {T[1]}, {m(1)}, {r0}, {T[1]}")
+            e(f"v_fma_f64 {T[1]}, {m(2)}, {i1}, {T[1]}")
+            e(f"v_fma_f64 {T[1]}, {m(3)}, {r1}, {T[1]}")
+            e(f"v_mul_f64 {T[2]}, {m(4)}, {r0}")
+            e(f"v_fma_f64 {T[2]}, -{m(5)}, {i0}, {T[2]}")
+            e(f"v_fma_f64 {T[2]}, {m(6)}, {r1}, {T[2]}")
+            e(f"v_fma_f64 {T[2]}, -{m(7)}, {i1}, {T[2]}")
+            e(f"v_mul_f64 {T[3]}, {m(4)}, {i0}")
+            e(f"v_fma_f64 {T[3]}, {m(5)}, {r0}, {T[3]}")
+            e(f"v_fma_f64 {T[3]}, {m(7)}, {r1}, {T[3]}")
+            e(f"v_fma_f64 {i1}, {m(6)}, {i1}, {T[3]}")
+            e(f"v_mov_b64 {r1}, {T[2]}")
+            e(f"v_mov_b64 {r0}, {T[0]}")
+            e(f"v_mov_b64 {i0}, {T[1]}")
+        elif kind == "M2R":   # m = m00 m01 m10 m11 (real)
+            e(f"v_mul_f64 {T[0]}, {m(0)}, {r0}")
+            e(f"v_fma_f64 {T[0]}, {m(1)}, {r1}, {T[0]}")
+            e(f"v_mul_f64 {T[1]}, {m(2)}, {r0}")
+            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[1]}")
+            e(f"v_mul_f64 {T[2]}, {m(0)}, {i0}")
+            e(f"v_fma_f64 {T[2]}, {m(1)}, {i1}, {T[2]}")
+            e(f"v_mul_f64 {T[3]}, {m(2)}, {i0}")
+            e(f"v_fma_f64 {i1}, {m(3)}, {i1}, {T[3]}")
+            e(f"v_mov_b64 {r0}, {T[0]}")
+            e(f"v_mov_b64 {i0}, {T[2]}")
+        elif kind == "M2RI":  # m = m00, Im m01, Im m10, m11
+            # a = m0 r0 - m1 i1 ; d = m3 i1 + m2 r0 ; b = m0 i0 + m1 r1 ; c = m3 r1 - m2 i0
+            e(f"v_mul_f64 {T[0]}, {m(0)}, {r0}")
+            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i1}, {T[0]}")
+            e(f"v_mul_f64 {T[1]}, {m(2)}, {r0}")
+            e(f"v_fma_f64 {i1}, {m(3)}, {i1}, {T[1]}")
+            e(f"v_mul_f64 {T[2]}, {m(0)}, {i0}")
+            e(f"v_fma_f64 {T[2]}, {m(1)}, {r1}, {T[2]}")
+            e(f"v_mul_f64 {T[3]}, -{m(2)}, {i0}")
+            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[3]}")
+            e(f"v_mov_b64 {r0}, {T[0]}")
+            e(f"v_mov_b64 {i0}, {T[2]}")
+        elif kind == "ANTI":  # m = m01 re,im ; m10 re,im
+            e(f"v_mul_f64 {T[0]}, {m(0)}, {r1}")
+            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i1}, {T[0]}")
+            e(f"v_mul_f64 {T[1]}, {m(0)}, {i1}")
+            e(f"v_fma_f64 {T[1]}, {m(1)}, {r1}, {T[1]}")
+            e(f"v_mul_f64 {r1}, {m(2)}, {r0}")
+            e(f"v_fma_f64 {r1}, -{m(3)}, {i0}, {r1}")
+            e(f"v_mul_f64 {i1}, {m(2)}, {i0}")
+            e(f"v_fma_f64 {i1}, {m(3)}, {r0}, {i1}")
+            e(f"v_mov_b64 {r0}, {T[0]}")
+            e(f"v_mov_b64 {i0}, {T[1]}")
+        elif kind == "SWAP":
+            for a, b in ((self.re(j), self.re(f)), (self.im(j), self.im(f))):
+                e(f"v_swap_b32 v{a}, v{b}")
+                e(f"v_swap_b32 v{a + 1}, v{b + 1}")
+        else:
+            raise ValueError(kind)
+
+    def cmul_sgpr(self, j, kr, ki):
+        # (x + iy) *= (m[kr] + i m[ki])
+        x, y = self.vp(self.re(j)), self.vp(self.im(j))
+        T = [self.vp(t) for t in self.T]
+        self.e(f"v_mul_f64 {T[0]}, {self.sm(ki)}, {y}")
+        self.e(f"v_mul_f64 {T[1]}, {self.sm(ki)}, {x}")
+        self.e(f"v_fma_f64 {x}, {self.sm(kr)}, {x}, -{T[0]}")
+        self.e(f"v_fma_f64 {y}, {self.sm(kr)}, {y}, {T[1]}")
+
+    def cmul_vgpr(self, j, cr, ci):
+        x, y = self.vp(self.re(j)), self.vp(self.im(j))
+        T = [self.vp(t) for t in self.T]
+        self.e(f"v_mul_f64 {T[0]}, {self.vp(ci)}, {y}")
+        self.e(f"v_mul_f64 {T[1]}, {self.vp(ci)}, {x}")
+        self.e(f"v_fma_f64 {x}, {self.vp(cr)}, {x}, -{T[0]}")
+        self.e(f"v_fma_f64 {y}, {self.vp(cr)}, {y}, {T[1]}")
+
+    # ---- handlers --------------------------------------------------------
+    def gen_slot(self, kind, s, ctrl):
+        self.handler(idx_slot(kind, s, ctrl), f"{kind}_s{s}_c{ctrl}")
+        if ctrl:
+            self.ctrl_begin()
+        for j in range(self.NS):
+            if (j >> s) & 1:
+                continue
+            f = j | (1 << s)
+            if ctrl:
+                skip = f".Lskip_{kind}_{s}_{j}"
+                self.ctrl_j(j, skip)
+                self.pair(kind, j, f)
+                self.label(skip)
+            else:
+                self.pair(kind, j, f)
+        if ctrl:
+            self.ctrl_end()
+        self.back()
+
+    def gen_d2s(self, s, ctrl):
+        self.handler(idx_d2s(s, ctrl), f"D2S_s{s}_c{ctrl}")
+        if ctrl:
+            self.ctrl_begin()
+        for j in range(self.NS):
+            one = (j >> s) & 1
+            if ctrl:
+                skip = f".Lskip_d2s_{s}_{j}"
+                self.ctrl_j(j, skip)
+                self.cmul_sgpr(j, 2 if one else 0, 3 if one else 1)
+                self.label(skip)
+            else:
+                self.cmul_sgpr(j, 2 if one else 0, 3 if one else 1)
+        if ctrl:
+            self.ctrl_end()
+        self.back()
+
+    def gen_d2l(self, ctrl):
+        self.handler(idx_d2l(ctrl), f"D2L_c{ctrl}")
+        # per-lane coefficient: lane bit aux (s71) ? d1 : d0
+        self.e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, s71, 1")
+        self.e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
+        C0, C1, T0, T1 = self.C0, self.C1, self.T[0], self.T[1]
+        self.e(f"v_mov_b64 {self.vp(C0)}, {self.sm(0)}")
+        self.e(f"v_mov_b64 {self.vp(C1)}, {self.sm(1)}")
+        self.e(f"v_mov_b64 {self.vp(T0)}, {self.sm(2)}")
+        self.e(f"v_mov_b64 {self.vp(T1)}, {self.sm(3)}")
+        for c, t in ((C0, T0), (C1, T1)):
+            self.e(f"v_cndmask_b32_e32 v{c}, v{c}, v{t}, vcc")
+            self.e(f"v_cndmask_b32_e32 v{c + 1}, v{c + 1}, v{t + 1}, vcc")
+        if ctrl:
+            self.ctrl_begin()
+        for j in range(self.NS):
+            if ctrl:
+                skip = f".Lskip_d2l_{j}"
+                self.ctrl_j(j, skip)
+                self.cmul_vgpr(j, C0, C1)
+                self.label(skip)
+            else:
+                self.cmul_vgpr(j, C0, C1)
+        if ctrl:
+            self.ctrl_end()
+        self.back()
+
+    def gen_diag(self):
+        self.handler(IDX_DIAG, "DIAG")
+        self.ctrl_begin()
+        for j in range(self.NS):
+            skip = f".Lskip_diag_{j}"
+            self.ctrl_j(j, skip)
+            self.cmul_sgpr(j, 0, 1)
+            self.label(skip)
+        self.ctrl_end()
+        self.back()
+
+    def gen_tr(self, s, l):
+        self.handler(idx_tr(s, l), f"TR_s{s}_l{l}")
+        e = self.e
+        e("s_nop 1")  # VALU write -> DPP / permlane read of the same VGPR
+        pairs = []
+        for j in range(self.NS):
+            if (j >> s) & 1:
+                continue
+            f = j | (1 << s)
+            for base in (self.re, self.im):
+                pairs.append((base(j), base(f)))
+                pairs.append((base(j) + 1, base(f) + 1))
+        tmp = [self.T[0], self.T[0] + 1, self.T[1], self.T[1] + 1, self.T[2], self.T[2] + 1, self.T[3], self.T[3] + 1]
+        if l >= 4:
+            op = "v_permlane32_swap_b32_e32" if l == 5 else "v_permlane16_swap_b32_e32"
+            for a, b in pairs:
+                e(f"{op} v{a}, v{b}")
+            self.back()
+            return
+        if l >= 2:
+            sh = 8 if l == 3 else 4
+            lo_banks = "0x3" if l == 3 else "0x5"   # lanes with the bit clear
+            hi_banks = "0xc" if l == 3 else "0xa"   # lanes with the bit set
+            for g in range(0, len(pairs), 4):
+                grp = pairs[g:g + 4]
+                for k, (a, b) in enumerate(grp):
+                    e(f"v_mov_b32_e32 v{tmp[k]}, v{b}")
+                e("s_nop 1")
+                for k, (a, b) in enumerate(grp):
+                    # bit clear: b <- partner(lane + sh).a ; bit set: a <- partner(lane - sh).b (old)
+                    e(f"v_mov_b32_dpp v{b}, v{a} row_shl:{sh} row_mask:0xf bank_mask:{lo_banks}")
+                    e(f"v_mov_b32_dpp v{a}, v{tmp[k]} row_shr:{sh} row_mask:0xf bank_mask:{hi_banks}")
+            self.back()
+            return
+        qp = "[1,0,3,2]" if l == 0 else "[2,3,0,1]"
+        e(f"v_and_b32_e32 v{self.vTmp}, {1 << l}, v{self.vLane}")
+        e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
+        for g in range(0, len(pairs), 4):
+            grp = pairs[g:g + 4]
+            for k, (a, b) in enumerate(grp):
+                e(f"v_mov_b32_dpp v{tmp[2 * k]}, v{b} quad_perm:{qp} row_mask:0xf bank_mask:0xf")
+                e(f"v_mov_b32_dpp v{tmp[2 * k + 1]}, v{a} quad_perm:{qp} row_mask:0xf bank_mask:0xf")
+            for k, (a, b) in enumerate(grp):
+                # bit set: a <- partner's b ; bit clear: b <- partner's a
+                e(f"v_cndmask_b32_e32 v{a}, v{a}, v{tmp[2 * k]}, vcc")
+                e(f"v_cndmask_b32_e32 v{b}, v{tmp[2 * k + 1]}, v{b}, vcc")
+            # the next group's DPPs read other registers: no hazard
+        self.back()
+
+    # ---- the kernel -------------------------------------------------------
+    def kernel(self):
+        R, NS, D = self.R, self.NS, self.D
+        NG = NS // 2       # 16-byte groups per array per lane
+        K = R + 6          # tile bits
+        L = self.lines
+        L.append('\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
+        L.append("\t.amdhsa_code_object_version 6")
+        L.append("\t.text")
+        L.append("\t.protected\tqa_wave_tile")
+        L.append("\t.globl\tqa_wave_tile")
+        L.append("\t.p2align\t8")
+        L.append("\t.type\tqa_wave_tile,@function")
+        self.label("qa_wave_tile")
+        e = self.e
+        vl, vldb, vstb, vt = self.vLane, self.vLdB, self.vStB, self.vTmp
+        e("s_load_dwordx4 s[4:7], s[0:1], 0x0")       # re, im
+        e("s_load_dwordx2 s[8:9], s[0:1], 0x10")      # launch record
+        e(f"v_and_b32_e32 v{vl}, 63, v0")     # one wave per workgroup
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_load_dwordx4 s[12:15], s[8:9], 0x0")     # numTiles, waveStride
+        e("s_load_dword s18, s[8:9], 0x10")           # nOps
+        e("s_load_dwordx8 s[20:27], s[8:9], 0x18")    # pos[0..7]
+        e("s_load_dwordx4 s[28:31], s[8:9], 0x38")    # pos[8..11]
+        e("s_add_u32 s10, s8, 1024")
+        e("s_addc_u32 s11, s9, 0")
+        e(f"v_lshlrev_b32_e32 v{vt}, 2, v{vl}")
+        e(f"global_load_dword v{vldb}, v{vt}, s[8:9] offset:344")
+        e(f"global_load_dword v{vstb}, v{vt}, s[8:9] offset:600")
+        # descriptor words 2,3 of the four quads
+        for q in (36, 40, 44, 48):
+            e(f"s_mov_b32 s{q + 2}, -1")
+            e(f"s_mov_b32 s{q + 3}, 0x20000")
+        # first tile = workgroup (one wave each)
+        e("s_mov_b32 s16, s2")
+        e("s_mov_b32 s17, 0")
+        e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.label(".Ltile_loop")
+        # tile < numTiles ?
+        e("s_sub_u32 s34, s16, s12")
+        e("s_subb_u32 s35, s17, s13")
+        e("s_cbranch_scc0 .Ldone")
+        # base = tile with zeros inserted at pos[0..K-1] (ascending)
+        e("s_mov_b64 s[32:33], s[16:17]")
+        for b in range(K):
+            p = f"s{20 + b}"
+            e(f"s_bfm_b64 s[96:97], {p}, 0")
+            e("s_and_b64 s[98:99], s[32:33], s[96:97]")
+            e(f"s_lshr_b64 s[32:33], s[32:33], {p}")
+            e(f"s_add_u32 s94, {p}, 1")
+            e("s_lshl_b64 s[32:33], s[32:33], s94")
+            e("s_or_b64 s[32:33], s[32:33], s[98:99]")
+        e("s_lshl_b64 s[34:35], s[32:33], 3")          # base in bytes
+        # loads: group jj of re / im, 16 B per lane
+        self.groups("ld", 88, vldb, NG)
+        e("s_waitcnt vmcnt(0)")
+        # ---- op loop
+        e("s_mov_b32 s19, 0")
+        e("s_mov_b64 s[94:95], s[10:11]")
+        self.label(".Lop_loop")
+        e("s_cmp_ge_u32 s19, s18")
+        e("s_cbranch_scc1 .Lops_done")
+        e("s_load_dwordx8 s[68:75], s[94:95], 0x0")
+        e("s_load_dwordx16 s[76:91], s[94:95], 0x20")
+        e("s_add_u32 s94, s94, 96")
+        e("s_addc_u32 s95, s95, 0")
+        e("s_add_u32 s19, s19, 1")
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_and_b64 s[96:97], s[32:33], s[72:73]")    # ctrlOut
+        e("s_cmp_eq_u64 s[96:97], s[72:73]")
+        e("s_cbranch_scc0 .Lop_loop")
+        e("s_getpc_b64 s[92:93]")
+        self.label("wave_anchor")
+        e("s_ashr_i32 s96, s68, 31")
+        e("s_add_u32 s92, s92, s68")
+        e("s_addc_u32 s93, s93, s96")
+        e("s_setpc_b64 s[92:93]")
+        self.label(".Lops_done")
+        self.groups("st", 216, vstb, NG)
+        e("s_add_u32 s16, s16, s14")
+        e("s_addc_u32 s17, s17, s15")
+        e("s_branch .Ltile_loop")
+        self.label(".Ldone")
+        e("s_endpgm")
+        # ---- handlers
+        for kind in KINDS:
+            for s in range(R):
+                for c in (0, 1):
+                    self.gen_slot(kind, s, c)
+        for s in range(R):
+            for c in (0, 1):
+                self.gen_d2s(s, c)
+        for c in (0, 1):
+            self.gen_d2l(c)
+        self.gen_diag()
+        for s in range(1, R):
+            for l in range(6):
+                self.gen_tr(s, l)
+        L.append(".Lfunc_end0:")
+        L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
+        self.descriptor()
+
+    def groups(self, what, off, vb, NG):
+        """Load or store the NG 16-byte groups of re and im (per lane)."""
+        e = self.e
+        # group byte offsets, 8 per s_load_dwordx16
+        for half in range(0, NG, 8):
+            n = min(8, NG - half)
+            dst = 52 if half == 0 else 68
+            e(f"s_load_dwordx16 s[{dst}:{dst + 15}], s[8:9], {off + 8 * half}")
+        e("s_waitcnt lgkmcnt(0)")
+        q = 0
+        for jj in range(NG):
+            g = (52 + 2 * jj) if jj < 8 else (68 + 2 * (jj - 8))
+            for arr, base in ((4, 2 * jj * 2), (6, 2 * self.NS + 2 * jj * 2)):
+                Q = (36, 40, 44, 48)[q % 4]
+                q += 1
+                e(f"s_add_u32 s{Q}, s{arr}, s34")
+                e(f"s_addc_u32 s{Q + 1}, s{arr + 1}, s35")
+                e(f"s_add_u32 s{Q}, s{Q}, s{g}")
+                e(f"s_addc_u32 s{Q + 1}, s{Q + 1}, s{g + 1}")
+                if what == "ld":
+                    e(f"buffer_load_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen nt")
+                else:
+                    e(f"buffer_store_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen nt")
+
+    def descriptor(self):
+        nv = self.nvgpr
+        nv8 = (nv + 7) // 8 * 8
+        L = self.lines
+        L.append("\t.section\t.rodata,\"a\",@progbits")
+        L.append("\t.p2align\t6, 0x0")
+        L.append("\t.amdhsa_kernel qa_wave_tile")
+        for k, v in [("group_segment_fixed_size", 0), ("private_segment_fixed_size", 0), ("kernarg_size", 24),
+                     ("user_sgpr_count", 2), ("user_sgpr_dispatch_ptr", 0), ("user_sgpr_queue_ptr", 0),
+                     ("user_sgpr_kernarg_segment_ptr", 1), ("user_sgpr_dispatch_id", 0),
+                     ("user_sgpr_kernarg_preload_length", 0), ("user_sgpr_kernarg_preload_offset", 0),
+                     ("user_sgpr_private_segment_size", 0), ("uses_dynamic_stack", 0),
+                     ("enable_private_segment", 0), ("system_sgpr_workgroup_id_x", 1),
+                     ("system_sgpr_workgroup_id_y", 0), ("system_sgpr_workgroup_id_z", 0),
+                     ("system_sgpr_workgroup_info", 0), ("system_vgpr_workitem_id", 0),
+                     ("next_free_vgpr", nv8), ("next_free_sgpr", 100), ("accum_offset", nv8),
+                     ("reserve_vcc", 1), ("float_round_mode_32", 0), ("float_round_mode_16_64", 0),
+                     ("float_denorm_mode_32", 3), ("float_denorm_mode_16_64", 3), ("dx10_clamp", 1),
+                     ("ieee_mode", 1), ("fp16_overflow", 0), ("tg_split", 0)]:
+            L.append(f"\t\t.amdhsa_{k} {v}")
+        L.append("\t.end_amdhsa_kernel")
+        L.append("\t.text")
+        L.append("\t.p2alignl 6, 3212836864")
+        L.append("\t.fill 256, 4, 3212836864")
+        L.append("\t.amdgpu_metadata")
+        L.append(f"""---
+amdhsa.kernels:
+  - .agpr_count:     0
+    .args:
+      - .address_space:  global
+        .offset:         0
+        .size:           8
+        .value_kind:     global_buffer
+      - .address_space:  global
+        .offset:         8
+        .size:           8
+        .value_kind:     global_buffer
+      - .address_space:  global
+        .offset:         16
+        .size:           8
+        .value_kind:     global_buffer
+    .group_segment_fixed_size: 0
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: 24
+    .language:       OpenCL C
+    .language_version:
+      - 2
+      - 0
+    .max_flat_workgroup_size: 64
+    .name:           qa_wave_tile
+    .private_segment_fixed_size: 0
+    .sgpr_count:     102
+    .sgpr_spill_count: 0
+    .symbol:         qa_wave_tile.kd
+    .uniform_work_group_size: 1
+    .uses_dynamic_stack: false
+    .vgpr_count:     {nv8}
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+amdhsa.target:   amdgcn-amd-amdhsa--gfx950
+amdhsa.version:
+  - 1
+  - 2
+...""")
+        L.append("\t.end_amdgpu_metadata")
+
+
+def elf_symbols(path):
+    """name -> value of the symbols of an ELF64 relocatable/shared object."""
+    data = open(path, "rb").read()
+    assert data[:4] == b"\x7fELF" and data[4] == 2
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    secs = []
+    for k in range(shnum):
+        name, typ, flags, addr, off, size, link, info, align, entsize = struct.unpack_from(
+            "<IIQQQQIIQQ", data, shoff + k * shentsize)
+        secs.append((name, typ, off, size, link, entsize))
+    out = {}
+    for name, typ, off, size, link, entsize in secs:
+        if typ != 2:  # SHT_SYMTAB
+            continue
+        stroff = secs[link][2]
+        for k in range(size // entsize):
+            st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from("<IBBHQQ", data,
+                                                                                          off + k * entsize)
+            end = data.index(b"\0", stroff + st_name)
+            out[data[stroff + st_name:end].decode()] = st_value
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["asm", "embed"])
+    ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--obj")
+    ap.add_argument("--hsaco")
+    args = ap.parse_args()
+    if args.mode == "asm":
+        g = Gen(args.slots)
+        g.kernel()
+        with open(args.out, "w") as f:
+            f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
+            f.write("\n".join(g.lines) + "\n")
+        # handler names per table index, for the embed step
+        with open(args.out + ".handlers", "w") as f:
+            for i in range(TABLE):
+                f.write(f"{i} {g.handlers.get(i, '-')}\n")
+        return
+    syms = elf_symbols(args.obj)
+    anchor = syms["wave_anchor"]
+    table = []
+    for line in open(args.out.replace("wave_image.inc", "wave_kernel.s") + ".handlers"):
+        i, name = line.split()
+        table.append(syms[name] - anchor if name != "-" else 0)
+    img = open(args.hsaco, "rb").read()
+    with open(args.out, "w") as f:
+        f.write("// GENERATED by tools/gen_wave_asm.py embed -- do not edit\n")
+        f.write(f"static const int kWaveImageSlots = {args.slots};\n")
+        f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
+        f.write(f"static const unsigned char kWaveImage[{len(img)}] __attribute__((aligned(4096))) = {{\n")
+        for k in range(0, len(img), 24):
+            f.write(", ".join(str(b) for b in img[k:k + 24]) + ",\n")
+        f.write("};\n")
+
+
+if __name__ == "__main__":
+    main()
