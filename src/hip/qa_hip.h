@@ -36,7 +36,7 @@ void setSyncWatchdog(void (*poll)(double elapsedSeconds));
 // runtime knobs (env QUEST_* at start-up, setQuESTTuning() afterwards)
 struct Tuning {
     int directKernels = 1;  // LDS-free kernels for single-op passes
-    int tileMode = 0;       // fused tiles: 0 op by op (default), 1 register phases, 2 dense blocks, 3 wave tiles
+    int tileMode = 0;       // fused tiles: 0 op by op, 1 register phases, 2 dense blocks, 3 wave tiles (fp64 default)
     int tileWgPerCU = 2;    // grid of the register-phase tile kernel, per CU
     int waveWgPerCU = 6;    // grid of the wave-tile kernel: waves per SIMD (one-wave workgroups)
     int directLayout = 1;   // direct kernels: 0 grid-stride units, 1 contiguous per workgroup

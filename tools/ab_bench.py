@@ -20,10 +20,11 @@ VARIANTS = {
     "fused-dense": dict(fusion=1, tile_mode=2, direct_kernels=1),
     "fused-opbyop": dict(fusion=1, tile_mode=0, direct_kernels=1),
     "fused-regphase": dict(fusion=1, tile_mode=1, direct_kernels=1),
+    "fused-wave": dict(fusion=1, tile_mode=3, direct_kernels=1),
     "eager-direct": dict(fusion=0, tile_mode=2, direct_kernels=1),
     "eager-tile": dict(fusion=0, tile_mode=2, direct_kernels=0),
 }
-DEFAULTS = {"tile_mode": 0, "direct_kernels": 1, "tile_wg_per_cu": 2, "fuse_blocks": 1, "tile_qubits": 0}
+DEFAULTS = {"tile_mode": 3, "direct_kernels": 1, "tile_wg_per_cu": 2, "fuse_blocks": 1, "tile_qubits": 0}
 
 
 def main():

@@ -47,14 +47,16 @@ def idx_d2l(ctrl):
     return 96 + ctrl
 
 
-IDX_DIAG = 98
-
-
 def idx_tr(s, l):
     return 100 + s * 6 + l                                 # 100..135
 
 
-TABLE = 136
+def idx_diag(creg, lane):
+    return 136 + creg * 2 + lane                           # 136..(136 + 2^(R+1))
+
+
+def table_size(R):
+    return 136 + (2 << R)
 
 
 class Gen:
@@ -62,7 +64,10 @@ class Gen:
         self.R = R
         self.NS = 1 << R
         self.lines = []
-        D = 4 * self.NS
+        # v[0 : 4NS) the tile being processed (A), v[4NS : 8NS) the next tile
+        # being loaded (B, software pipeline), then temporaries
+        self.B = 4 * self.NS
+        D = 8 * self.NS
         self.D = D
         self.T = [D + 0, D + 2, D + 4, D + 6]   # temporaries (double pairs)
         self.C0, self.C1 = D + 8, D + 10
@@ -99,7 +104,29 @@ class Gen:
         self.label(lab)
 
     def back(self):
-        self.e("s_branch .Lop_loop")
+        self.next_op()
+
+    def next_op(self):
+        """Start the next op (inlined at the end of every handler: one taken
+        branch per op).  Op k+1's record was prefetched into s[36:59] while op
+        k ran; it is moved to s[68:91] and op k+2 is prefetched."""
+        e = self.e
+        e("s_cmp_ge_u32 s19, s18")
+        e("s_cbranch_scc1 .Lops_done")
+        e("s_waitcnt lgkmcnt(0)")
+        for k in range(0, 24, 2):
+            e(f"s_mov_b64 s[{68 + k}:{69 + k}], s[{36 + k}:{37 + k}]")
+        e("s_add_u32 s19, s19, 1")
+        e("s_add_u32 s94, s94, 96")
+        e("s_addc_u32 s95, s95, 0")
+        e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
+        e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
+        e("s_and_b64 s[96:97], s[32:33], s[72:73]")    # ctrlOut of the op
+        e("s_cmp_eq_u64 s[96:97], s[72:73]")
+        e("s_cbranch_scc0 .Lnext")
+        e("s_add_u32 s98, s92, s68")                   # kernel base + handler offset
+        e("s_addc_u32 s99, s93, 0")
+        e("s_setpc_b64 s[98:99]")
 
     # ---- predication: per register j, exec = lanes whose controls hold ----
     def ctrl_begin(self):
@@ -112,8 +139,7 @@ class Gen:
         # exec = (j & cReg) == cReg ? LM : 0
         self.e(f"s_and_b32 s98, s69, {j}")
         self.e("s_cmp_eq_u32 s98, s69")
-        self.e("s_cselect_b64 s[98:99], s[96:97], 0")
-        self.e("s_mov_b64 exec, s[98:99]")
+        self.e("s_cselect_b64 exec, s[96:97], 0")
         self.e(f"s_cbranch_execz {skip}")
 
     def ctrl_end(self):
@@ -267,15 +293,30 @@ class Gen:
             self.ctrl_end()
         self.back()
 
-    def gen_diag(self):
-        self.handler(IDX_DIAG, "DIAG")
-        self.ctrl_begin()
-        for j in range(self.NS):
-            skip = f".Lskip_diag_{j}"
-            self.ctrl_j(j, skip)
-            self.cmul_sgpr(j, 0, 1)
-            self.label(skip)
-        self.ctrl_end()
+    def gen_diag(self, creg, lane):
+        """Phase m[0] + i m[1] on the registers j with (j & creg) == creg
+        (chosen here, at generation time) of the lanes whose cLane bits are 1
+        (lane = 1: per-lane phase, 1 on the other lanes)."""
+        self.handler(idx_diag(creg, lane), f"DIAG_m{creg}_l{lane}")
+        e = self.e
+        js = [j for j in range(self.NS) if (j & creg) == creg]
+        if not lane:
+            for j in js:
+                self.cmul_sgpr(j, 0, 1)
+            self.back()
+            return
+        C0, C1 = self.C0, self.C1
+        e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
+        e(f"v_cmp_eq_u32_e32 vcc, s70, v{self.vTmp}")
+        e(f"v_mov_b64 {self.vp(C0)}, {self.sm(0)}")
+        e(f"v_mov_b64 {self.vp(C1)}, {self.sm(1)}")
+        e(f"v_cndmask_b32_e32 v{C0}, 0, v{C0}, vcc")
+        e(f"v_mov_b32_e32 v{self.vTmp}, 0x3ff00000")   # hi dword of 1.0 (literal + vcc: two constant-bus reads)
+        e(f"v_cndmask_b32_e32 v{C0 + 1}, v{self.vTmp}, v{C0 + 1}, vcc")
+        e(f"v_cndmask_b32_e32 v{C1}, 0, v{C1}, vcc")
+        e(f"v_cndmask_b32_e32 v{C1 + 1}, 0, v{C1 + 1}, vcc")
+        for j in js:
+            self.cmul_vgpr(j, C0, C1)
         self.back()
 
     def gen_tr(self, s, l):
@@ -346,6 +387,10 @@ class Gen:
         e("s_load_dwordx4 s[4:7], s[0:1], 0x0")       # re, im
         e("s_load_dwordx2 s[8:9], s[0:1], 0x10")      # launch record
         e(f"v_and_b32_e32 v{vl}, 63, v0")     # one wave per workgroup
+        e("s_getpc_b64 s[92:93]")
+        self.label(".Lentry_pc")
+        e("s_sub_u32 s92, s92, .Lentry_pc-qa_wave_tile")   # kernel base: handlers jump from here
+        e("s_subb_u32 s93, s93, 0")
         e("s_waitcnt lgkmcnt(0)")
         e("s_load_dwordx4 s[12:15], s[8:9], 0x0")     # numTiles, waveStride
         e("s_load_dword s18, s[8:9], 0x10")           # nOps
@@ -356,58 +401,44 @@ class Gen:
         e(f"v_lshlrev_b32_e32 v{vt}, 2, v{vl}")
         e(f"global_load_dword v{vldb}, v{vt}, s[8:9] offset:344")
         e(f"global_load_dword v{vstb}, v{vt}, s[8:9] offset:600")
-        # descriptor words 2,3 of the four quads
-        for q in (36, 40, 44, 48):
-            e(f"s_mov_b32 s{q + 2}, -1")
-            e(f"s_mov_b32 s{q + 3}, 0x20000")
         # first tile = workgroup (one wave each)
         e("s_mov_b32 s16, s2")
         e("s_mov_b32 s17, 0")
         e("s_waitcnt vmcnt(0) lgkmcnt(0)")
-        self.label(".Ltile_loop")
-        # tile < numTiles ?
-        e("s_sub_u32 s34, s16, s12")
-        e("s_subb_u32 s35, s17, s13")
-        e("s_cbranch_scc0 .Ldone")
-        # base = tile with zeros inserted at pos[0..K-1] (ascending)
-        e("s_mov_b64 s[32:33], s[16:17]")
-        for b in range(K):
-            p = f"s{20 + b}"
-            e(f"s_bfm_b64 s[96:97], {p}, 0")
-            e("s_and_b64 s[98:99], s[32:33], s[96:97]")
-            e(f"s_lshr_b64 s[32:33], s[32:33], {p}")
-            e(f"s_add_u32 s94, {p}, 1")
-            e("s_lshl_b64 s[32:33], s[32:33], s94")
-            e("s_or_b64 s[32:33], s[32:33], s[98:99]")
-        e("s_lshl_b64 s[34:35], s[32:33], 3")          # base in bytes
-        # loads: group jj of re / im, 16 B per lane
-        self.groups("ld", 88, vldb, NG)
+        # Software pipeline: while the ops run on tile i (registers A), tile
+        # i+1 is already loading into registers B; at the top of iteration
+        # i+1 B is copied to A.  Prologue: load the first tile into B.
+        self.tile_check("s[16:17]", ".Ldone")
+        self.base_of("s[16:17]", 68)
+        self.groups("ld", 88, vldb, NG, self.B, 70)
         e("s_waitcnt vmcnt(0)")
-        # ---- op loop
+        e("s_branch .Lcopy")
+        self.label(".Ltile_loop")
+        e(f"s_waitcnt vmcnt({2 * NG})")   # tile i+1's loads are older than tile i's stores
+        self.label(".Lcopy")
+        for r in range(0, 4 * NS, 2):
+            e(f"v_mov_b64 v[{r}:{r + 1}], v[{self.B + r}:{self.B + r + 1}]")
+        self.base_of("s[16:17]", 32)     # this tile: ctrlOut tests and stores
+        # prefetch the next tile into B
+        e("s_add_u32 s72, s16, s14")
+        e("s_addc_u32 s73, s17, s15")
+        self.tile_check("s[72:73]", ".Lno_prefetch")
+        self.base_of("s[72:73]", 68)
+        self.groups("ld", 88, vldb, NG, self.B, 70)
+        self.label(".Lno_prefetch")
+        # ---- op loop: prefetch op 0, then every op starts through next_op()
         e("s_mov_b32 s19, 0")
         e("s_mov_b64 s[94:95], s[10:11]")
-        self.label(".Lop_loop")
-        e("s_cmp_ge_u32 s19, s18")
-        e("s_cbranch_scc1 .Lops_done")
-        e("s_load_dwordx8 s[68:75], s[94:95], 0x0")
-        e("s_load_dwordx16 s[76:91], s[94:95], 0x20")
-        e("s_add_u32 s94, s94, 96")
-        e("s_addc_u32 s95, s95, 0")
-        e("s_add_u32 s19, s19, 1")
-        e("s_waitcnt lgkmcnt(0)")
-        e("s_and_b64 s[96:97], s[32:33], s[72:73]")    # ctrlOut
-        e("s_cmp_eq_u64 s[96:97], s[72:73]")
-        e("s_cbranch_scc0 .Lop_loop")
-        e("s_getpc_b64 s[92:93]")
-        self.label("wave_anchor")
-        e("s_ashr_i32 s96, s68, 31")
-        e("s_add_u32 s92, s92, s68")
-        e("s_addc_u32 s93, s93, s96")
-        e("s_setpc_b64 s[92:93]")
+        e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
+        e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
+        self.label(".Lnext")
+        self.next_op()
         self.label(".Lops_done")
-        self.groups("st", 216, vstb, NG)
+        e("s_waitcnt lgkmcnt(0)")      # the prefetch past the last op writes s[36:59]
+        self.groups("st", 216, vstb, NG, 0, 34)
         e("s_add_u32 s16, s16, s14")
         e("s_addc_u32 s17, s17, s15")
+        self.tile_check("s[16:17]", ".Ldone")
         e("s_branch .Ltile_loop")
         self.label(".Ldone")
         e("s_endpgm")
@@ -421,7 +452,9 @@ class Gen:
                 self.gen_d2s(s, c)
         for c in (0, 1):
             self.gen_d2l(c)
-        self.gen_diag()
+        for creg in range(self.NS):
+            for lane in (0, 1):
+                self.gen_diag(creg, lane)
         for s in range(1, R):
             for l in range(6):
                 self.gen_tr(s, l)
@@ -429,23 +462,51 @@ class Gen:
         L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
         self.descriptor()
 
-    def groups(self, what, off, vb, NG):
-        """Load or store the NG 16-byte groups of re and im (per lane)."""
+    def tile_check(self, tile, done):
+        """Branch to `done` unless tile < numTiles (s[12:13])."""
+        lo = int(tile[2:tile.index(":")])
+        self.e(f"s_sub_u32 s98, s{lo}, s12")
+        self.e(f"s_subb_u32 s99, s{lo + 1}, s13")
+        self.e(f"s_cbranch_scc0 {done}")
+
+    def base_of(self, tile, d):
+        """s[d:d+1] = tile index with zeros inserted at pos[0..K-1] (ascending),
+        s[d+2:d+3] = the same in bytes."""
+        e = self.e
+        e(f"s_mov_b64 s[{d}:{d + 1}], {tile}")
+        for b in range(self.R + 6):
+            p = f"s{20 + b}"
+            e(f"s_bfm_b64 s[96:97], {p}, 0")
+            e(f"s_and_b64 s[98:99], s[{d}:{d + 1}], s[96:97]")
+            e(f"s_lshr_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], {p}")
+            e(f"s_add_u32 s94, {p}, 1")
+            e(f"s_lshl_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s94")
+            e(f"s_or_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s[98:99]")
+        e(f"s_lshl_b64 s[{d + 2}:{d + 3}], s[{d}:{d + 1}], 3")
+
+    def groups(self, what, off, vb, NG, regbase, bpair):
+        """Load or store the NG 16-byte groups of re and im (per lane) of the
+        register set at `regbase`, tile base in bytes in s[bpair:bpair+1]."""
         e = self.e
         # group byte offsets, 8 per s_load_dwordx16
         for half in range(0, NG, 8):
             n = min(8, NG - half)
             dst = 52 if half == 0 else 68
             e(f"s_load_dwordx16 s[{dst}:{dst + 15}], s[8:9], {off + 8 * half}")
+        # descriptor words 2,3 of the four quads (s[36:59] also holds the
+        # prefetched op record during the op loop)
+        for Q in (36, 40, 44, 48):
+            e(f"s_mov_b32 s{Q + 2}, -1")
+            e(f"s_mov_b32 s{Q + 3}, 0x20000")
         e("s_waitcnt lgkmcnt(0)")
         q = 0
         for jj in range(NG):
             g = (52 + 2 * jj) if jj < 8 else (68 + 2 * (jj - 8))
-            for arr, base in ((4, 2 * jj * 2), (6, 2 * self.NS + 2 * jj * 2)):
+            for arr, base in ((4, regbase + 2 * jj * 2), (6, regbase + 2 * self.NS + 2 * jj * 2)):
                 Q = (36, 40, 44, 48)[q % 4]
                 q += 1
-                e(f"s_add_u32 s{Q}, s{arr}, s34")
-                e(f"s_addc_u32 s{Q + 1}, s{arr + 1}, s35")
+                e(f"s_add_u32 s{Q}, s{arr}, s{bpair}")
+                e(f"s_addc_u32 s{Q + 1}, s{arr + 1}, s{bpair + 1}")
                 e(f"s_add_u32 s{Q}, s{Q}, s{g}")
                 e(f"s_addc_u32 s{Q + 1}, s{Q + 1}, s{g + 1}")
                 if what == "ld":
@@ -560,11 +621,11 @@ def main():
             f.write("\n".join(g.lines) + "\n")
         # handler names per table index, for the embed step
         with open(args.out + ".handlers", "w") as f:
-            for i in range(TABLE):
+            for i in range(table_size(args.slots)):
                 f.write(f"{i} {g.handlers.get(i, '-')}\n")
         return
     syms = elf_symbols(args.obj)
-    anchor = syms["wave_anchor"]
+    anchor = syms["qa_wave_tile"]
     table = []
     for line in open(args.out.replace("wave_image.inc", "wave_kernel.s") + ".handlers"):
         i, name = line.split()

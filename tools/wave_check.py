@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--modes", default="0,3")
     ap.add_argument("--skip-check", action="store_true")
+    ap.add_argument("--wg", default="", help="comma list of wave_wg_per_cu values to time (mode 3)")
     args = ap.parse_args()
     import quest_amd as qa
     from quest_amd.models import random_layered
@@ -62,14 +63,19 @@ def main():
 
     n = args.qubits
     modes = [int(m) for m in args.modes.split(",")]
+    variants = [(m, None) for m in modes]
+    if args.wg:
+        variants = [(3, int(w)) for w in args.wg.split(",")]
     reg = qa.Register(env, n)
     reg.init_plus()
     circ = random_layered(n, args.layers, seed=7)
-    times = {m: [] for m in modes}
+    times = {v: [] for v in variants}
     stats = {}
     for r in range(args.rounds):
-        for m in modes:
-            capi.setQuESTTuning("tile_mode", m)
+        for m in variants:
+            capi.setQuESTTuning("tile_mode", m[0])
+            if m[1] is not None:
+                capi.setQuESTTuning("wave_wg_per_cu", m[1])
             reg.sync()
             capi.resetQuESTStats()
             t0 = time.perf_counter()
@@ -78,9 +84,9 @@ def main():
             times[m].append(time.perf_counter() - t0)
             stats[m] = capi.getQuESTStats()
     g = len(circ.gates)
-    for m in modes:
+    for m in variants:
         best = min(times[m])
-        print(f"mode {m}: {1e3 * best / g:.4f} ms/gate ({1e3 * best / args.layers:.2f} ms/layer) "
+        print(f"mode {m[0]} wg {m[1]}: {1e3 * best / g:.4f} ms/gate ({1e3 * best / args.layers:.2f} ms/layer) "
               f"passes {stats[m]['passes']} wave {stats[m]['wavePasses']} all {[round(1e3 * t, 1) for t in times[m]]}",
               flush=True)
     print("norm", reg.total_prob())
