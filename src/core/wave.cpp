@@ -35,7 +35,7 @@ M2Class classify(const real* m) {
 struct Layout {
     int where[kWaveBits];
     int slotBit[kWaveSlots];
-    int laneBit[kWaveLanes];
+    int laneBit[kWaveLaneBits];
 
     void put(int b, int w) {
         where[b] = w;
@@ -67,7 +67,7 @@ WaveOp blank(int kind) {
 
 }  // namespace
 
-int waveTransposeCost(int laneBit) { return laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
+int waveTransposeCost(int laneBit) { return laneBit >= kWaveLanes ? 3 : laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
 
 bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out) {
     if (ps.k != kWaveBits) return false;
@@ -101,19 +101,40 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     for (int l = 0; l < 3; l++) lay.put(l + 1, kWaveSlots + l);
     std::vector<int> high;
     for (int b = 4; b < kWaveBits; b++) high.push_back(b);
-    // bits above kWaveLanePosMax must take slots; then earliest need first
+    // bits above kWaveLanePosMax may not sit on real lanes (32-bit per-lane
+    // offsets); wave bits take any position (per-wave uniform offsets)
     auto farPos = [&](int b) { return ps.pos[b] > kWaveLanePosMax; };
     int nFar = 0;
     for (int b : high) nFar += farPos(b);
-    if (nFar > kWaveSlots - 1) return false;
-    std::stable_sort(high.begin(), high.end(), [&](int x, int y) {
-        if (farPos(x) != farPos(y)) return farPos(x);
-        return nextUse(0, x) < nextUse(0, y);
-    });
-    for (int s = 1; s < kWaveSlots; s++) lay.put(high[s - 1], s);
-    for (int l = 3; l < kWaveLanes; l++) lay.put(high[kWaveSlots - 1 + l - 3], kWaveSlots + l);
+    if (nFar > (kWaveSlots - 1) + kWaveWBits) return false;
+    // slots: the bits needed in a slot earliest; then real lanes 3-5 for the
+    // next near bits, wave bits for the rest (LDS transpositions are dearest)
+    std::stable_sort(high.begin(), high.end(), [&](int x, int y) { return nextUse(0, x) < nextUse(0, y); });
+    std::vector<int> slots(high.begin(), high.begin() + (kWaveSlots - 1));
+    std::vector<int> rest(high.begin() + (kWaveSlots - 1), high.end());
+    // real lanes 3-5: three near bits, from the rest first (in need order);
+    // if the rest has fewer, near bits leave the slots for them and far bits
+    // of the rest take their slot places
+    std::vector<int> lanes, waves;
+    for (int b : rest)
+        if (!farPos(b) && (int)lanes.size() < kWaveLanes - 3) lanes.push_back(b);
+        else waves.push_back(b);
+    for (int k = (int)slots.size() - 1; k >= 0 && (int)lanes.size() < kWaveLanes - 3; k--) {
+        if (farPos(slots[k])) continue;
+        int far = -1;
+        for (int x = 0; x < (int)waves.size() && far < 0; x++)
+            if (farPos(waves[x])) far = x;
+        if (far < 0) return false;
+        lanes.push_back(slots[k]);
+        slots[k] = waves[far];
+        waves.erase(waves.begin() + far);
+    }
+    if ((int)lanes.size() != kWaveLanes - 3 || (int)waves.size() != kWaveWBits) return false;
+    for (int s = 1; s < kWaveSlots; s++) lay.put(slots[s - 1], s);
+    for (int l = 3; l < kWaveLanes; l++) lay.put(lanes[l - 3], kWaveSlots + l);
+    for (int l = kWaveLanes; l < kWaveLaneBits; l++) lay.put(waves[l - kWaveLanes], kWaveSlots + l);
     for (int s = 0; s < kWaveSlots; s++) wp.ldSlot[s] = lay.slotBit[s];
-    for (int l = 0; l < kWaveLanes; l++) wp.ldLane[l] = lay.laneBit[l];
+    for (int l = 0; l < kWaveLaneBits; l++) wp.ldLane[l] = lay.laneBit[l];
 
     wp.opBegin = (int)out.ops.size();
     auto transpose = [&](int s, int l) {
@@ -146,6 +167,20 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 masks(lay, op.ctrlIn | (1u << t), w.cReg, w.cLane);
                 w.m[0] = m[6];
                 w.m[1] = m[7];
+            } else if (!inSlot(lay.where[t]) && laneOf(lay.where[t]) >= kWaveLanes) {
+                // target on a wave bit: d1 on the waves with the bit set, d0
+                // on the others (two wave-uniform phase ops)
+                const unsigned wb = 1u << laneOf(lay.where[t]);
+                for (int v = 0; v < 2; v++) {
+                    WaveOp d = blank((int)WKind::DIAG);
+                    masks(lay, op.ctrlIn, d.cReg, d.cLane);
+                    if (v) d.cLane |= wb; else d.cLaneZero |= wb;
+                    d.m[0] = m[v ? 6 : 0];
+                    d.m[1] = m[v ? 7 : 1];
+                    d.ctrlOut = op.ctrlOut;
+                    out.ops.push_back(d);
+                }
+                continue;
             } else {
                 const int wt = lay.where[t];
                 w = blank(inSlot(wt) ? (int)WKind::D2S : (int)WKind::D2L);
@@ -220,7 +255,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             transpose(1, l);
         }
     }
-    // lane bits 3.. may not carry positions above kWaveLanePosMax at store
+    // real lane bits 3.. may not carry positions above kWaveLanePosMax at store
     for (int l = 3; l < kWaveLanes; l++) {
         if (!farPos(lay.laneBit[l])) continue;
         int s = -1;
@@ -230,7 +265,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         transpose(s, l);
     }
     for (int s = 0; s < kWaveSlots; s++) wp.stSlot[s] = lay.slotBit[s];
-    for (int l = 0; l < kWaveLanes; l++) wp.stLane[l] = lay.laneBit[l];
+    for (int l = 0; l < kWaveLaneBits; l++) wp.stLane[l] = lay.laneBit[l];
     wp.opEnd = (int)out.ops.size();
     out.passes.push_back(wp);
     stats().waveOps += wp.opEnd - wp.opBegin;

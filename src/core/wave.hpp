@@ -39,7 +39,15 @@ namespace qa {
 // loop-carried tile in registers (spills at any occupancy)
 constexpr int kWaveSlots = QA_WAVE_SLOTS;
 constexpr int kWaveLanes = 6;   // 64 lanes
-constexpr int kWaveBits = kWaveSlots + kWaveLanes;
+// A tile is shared by 2^kWaveWBits waves of a workgroup: "wave bits" are
+// virtual lane bits 6.. of the tile (transpositions with a slot go through
+// LDS, controls on them are wave-uniform predicates)
+#ifndef QA_WAVE_WBITS
+#define QA_WAVE_WBITS 2
+#endif
+constexpr int kWaveWBits = QA_WAVE_WBITS;
+constexpr int kWaveLaneBits = kWaveLanes + kWaveWBits;  // real + wave lane bits
+constexpr int kWaveBits = kWaveSlots + kWaveLaneBits;
 constexpr int kWaveLanePosMax = 27;
 
 enum class WKind : int {
@@ -51,7 +59,7 @@ enum class WKind : int {
     DIAG = 5,  // multiply every element whose (cReg, cLane) bits are 1 by m[0] + i m[1]
     D2S = 6,   // diagonal 2x2 on the bit of slot a (m = d0 re,im, d1 re,im)
     D2L = 7,   // diagonal 2x2 on lane bit a
-    TR = 8,    // transpose slot a with lane bit b (never masked)
+    TR = 8,    // transpose slot a with lane bit b (b >= 6: wave bit, through LDS; never masked)
 };
 
 // One op, uploaded as-is (uniform: read through the scalar cache).
@@ -59,8 +67,8 @@ struct WaveOp {
     int kind;
     int a, b;
     unsigned cReg;    // register slots that must be 1
-    unsigned cLane;   // lane bits that must be 1
-    int pad;
+    unsigned cLane;   // lane bits that must be 1 (bits >= 6: wave bits)
+    unsigned cLaneZero;  // lane bits that must be 0 (wave bits only)
     u64 ctrlOut;      // physical bits outside the tile that must be 1
     real m[8];
 };
@@ -69,9 +77,9 @@ struct WavePass {
     int pos[kWaveBits];        // tile bit -> physical position (pos[i] = i for i < 4)
     int opBegin = 0, opEnd = 0;
     int ldSlot[kWaveSlots];    // tile bit held by slot s at load
-    int ldLane[kWaveLanes];    // tile bit held by lane bit l at load
+    int ldLane[kWaveLaneBits]; // tile bit held by lane bit l at load (l >= 6: wave bits)
     int stSlot[kWaveSlots];    // ... at store
-    int stLane[kWaveLanes];
+    int stLane[kWaveLaneBits];
 };
 
 struct WaveProgram {

@@ -308,10 +308,11 @@ void runTilePass(real* re, real* im, int L, const TileProgram& prog, const TileP
     }
 }
 
-// Wave-tile emulation: 64 "lanes" x 32 register slots per tile, exactly the
+// Wave-tile emulation: 64 lanes x waves x 2^kWaveSlots registers per tile, exactly the
 // data movement of the GPU wave kernel (src/hip/kernels_wave.hip), so the
 // planner's transpositions and layouts are validated on CPU.
 constexpr int kWaveRegs = 1 << kWaveSlots;
+constexpr int kVLanes = 1 << kWaveLaneBits;  // 64 lanes x the waves sharing a tile
 
 void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) {
     const WKind kind = (WKind)w.kind;
@@ -320,7 +321,7 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         for (int j = 0; j < kWaveRegs; j++) {
             if ((j >> s) & 1) continue;
             const int f = j | (1 << s);
-            for (int L0 = 0; L0 < 64; L0++) {
+            for (int L0 = 0; L0 < kVLanes; L0++) {
                 if ((L0 >> l) & 1) continue;
                 const int L1 = L0 | (1 << l);
                 std::swap(vr[L1][j], vr[L0][f]);
@@ -330,8 +331,9 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         return;
     }
     const real* m = w.m;
-    for (int lane = 0; lane < 64; lane++) {
+    for (int lane = 0; lane < kVLanes; lane++) {
         if (((unsigned)lane & w.cLane) != w.cLane) continue;
+        if ((unsigned)lane & w.cLaneZero) continue;
         real* r = vr[lane];
         real* i = vi[lane];
         if (kind == WKind::DIAG || kind == WKind::D2S || kind == WKind::D2L) {
@@ -390,16 +392,16 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
 }
 
 void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {
-    static thread_local i64 ld[64][kWaveRegs], st[64][kWaveRegs];
+    static thread_local i64 ld[kVLanes][kWaveRegs], st[kVLanes][kWaveRegs];
     auto offsetOf = [&](const int* slotBit, const int* laneBit, int lane, int j) {
         i64 off = 0;
         for (int s = 0; s < kWaveSlots; s++)
             if ((j >> s) & 1) off |= (i64)1 << ps.pos[slotBit[s]];
-        for (int l = 0; l < kWaveLanes; l++)
+        for (int l = 0; l < kWaveLaneBits; l++)
             if ((lane >> l) & 1) off |= (i64)1 << ps.pos[laneBit[l]];
         return off;
     };
-    for (int lane = 0; lane < 64; lane++)
+    for (int lane = 0; lane < kVLanes; lane++)
         for (int j = 0; j < kWaveRegs; j++) {
             ld[lane][j] = offsetOf(ps.ldSlot, ps.ldLane, lane, j);
             st[lane][j] = offsetOf(ps.stSlot, ps.stLane, lane, j);
@@ -410,13 +412,13 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
     const i64 tiles = (i64)1 << (L - kWaveBits);
 #pragma omp parallel if (((i64)1 << L) >= kOmpMin)
     {
-        std::vector<real> bufR(64 * kWaveRegs), bufI(64 * kWaveRegs);
+        std::vector<real> bufR(kVLanes * kWaveRegs), bufI(kVLanes * kWaveRegs);
         real(*vr)[kWaveRegs] = reinterpret_cast<real(*)[kWaveRegs]>(bufR.data());
         real(*vi)[kWaveRegs] = reinterpret_cast<real(*)[kWaveRegs]>(bufI.data());
 #pragma omp for schedule(static)
         for (i64 T = 0; T < tiles; T++) {
             const i64 base = tileBase(tp, T, L);
-            for (int lane = 0; lane < 64; lane++)
+            for (int lane = 0; lane < kVLanes; lane++)
                 for (int j = 0; j < kWaveRegs; j++) {
                     vr[lane][j] = re[base + ld[lane][j]];
                     vi[lane][j] = im[base + ld[lane][j]];
@@ -426,7 +428,7 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
                 if (((u64)base & w.ctrlOut) != w.ctrlOut) continue;
                 applyWaveOp(w, vr, vi);
             }
-            for (int lane = 0; lane < 64; lane++)
+            for (int lane = 0; lane < kVLanes; lane++)
                 for (int j = 0; j < kWaveRegs; j++) {
                     re[base + st[lane][j]] = vr[lane][j];
                     im[base + st[lane][j]] = vi[lane][j];

@@ -30,6 +30,7 @@ Semantics of every op: src/core/wave.hpp (and the CPU emulation in
 src/cpu/backend_cpu.cpp applyWaveOp, which the tests compare against).
 """
 import argparse
+import re
 import struct
 import sys
 
@@ -55,29 +56,145 @@ def idx_diag(creg, lane):
     return 136 + creg * 2 + lane                           # 136..(136 + 2^(R+1))
 
 
+def idx_trw(s, b):
+    return 200 + s * 2 + b                                 # 200..(200 + 2R)
+
+
 def table_size(R):
-    return 136 + (2 << R)
+    return max(136 + (2 << R), 216)
+
+
+_VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b|\b(vcc)\b")
+
+
+def _regs(operand):
+    out = set()
+    for m in _VREG.finditer(operand):
+        if m.group(1):
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+        elif m.group(3):
+            out.add(int(m.group(3)))
+        else:
+            out.add("vcc")
+    return out
+
+
+def schedule(body):
+    """List-schedule a straight-line VALU region: keep every RAW / WAR / WAW
+    order of the program, otherwise issue the longest-critical-path
+    instruction whose operands are ready (fp64 results assumed ready 3 issue
+    slots later, others 2) -- interleaves the independent FMA chains of
+    different pairs / elements instead of stalling on each chain."""
+    n = len(body)
+    defs, uses, lat = [], [], []
+    for ins in body:
+        op, _, rest = ins.partition(" ")
+        ops = [x.strip() for x in rest.split(",")] if rest else []
+        d = _regs(ops[0]) if ops else set()
+        u = set()
+        for x in ops[1:]:
+            u |= _regs(x)
+        if op.startswith("v_swap"):
+            u |= d | _regs(ops[1])
+            d = d | _regs(ops[1])
+        if op.startswith("v_cndmask_b32_e32"):
+            u.add("vcc")
+        if op.startswith("v_fmac"):
+            u |= d
+        defs.append(d)
+        uses.append(u)
+        lat.append(3 if "f64" in op else 2)
+    preds = [dict() for _ in range(n)]   # pred -> delay
+    last_w, readers = {}, {}
+    for i in range(n):
+        for r in uses[i]:
+            if r in last_w:
+                w = last_w[r]
+                preds[i][w] = max(preds[i].get(w, 0), lat[w])
+        for r in defs[i]:
+            for rd in readers.get(r, ()):
+                if rd != i:
+                    preds[i][rd] = max(preds[i].get(rd, 0), 1)
+            if r in last_w and last_w[r] != i:
+                preds[i][last_w[r]] = max(preds[i].get(last_w[r], 0), 1)
+        for r in uses[i]:
+            readers.setdefault(r, []).append(i)
+        for r in defs[i]:
+            last_w[r] = i
+            readers[r] = []
+    succs = [[] for _ in range(n)]
+    for i in range(n):
+        for p in preds[i]:
+            succs[p].append(i)
+    crit = [0] * n
+    for i in range(n - 1, -1, -1):
+        crit[i] = lat[i] + max((crit[s] for s in succs[i]), default=0)
+    done = [False] * n
+    at = [0] * n
+    left = [len(preds[i]) for i in range(n)]
+    ready = [i for i in range(n) if left[i] == 0]
+    out, t = [], 0
+    while ready:
+        def earliest(i):
+            return max((at[p] + d for p, d in preds[i].items()), default=0)
+        avail = [i for i in ready if earliest(i) <= t]
+        if not avail:
+            t = min(earliest(i) for i in ready)
+            continue
+        i = max(avail, key=lambda k: (crit[k], -k))
+        ready.remove(i)
+        done[i] = True
+        at[i] = t
+        out.append(body[i])
+        t += 1
+        for s2 in succs[i]:
+            left[s2] -= 1
+            if left[s2] == 0:
+                ready.append(s2)
+    assert len(out) == n
+    return out
 
 
 class Gen:
-    def __init__(self, R):
+    def __init__(self, R, dbuf, W, debug=False):
+        self.debug = debug
         self.R = R
         self.NS = 1 << R
+        self.dbuf = dbuf
+        self.W = W               # wave bits: 2^W waves share a tile (LDS exchanges)
+        self.NW = 1 << W
+        self.OUTBOX = self.NS * 512   # bytes of one wave's LDS outbox (NS doubles x 64 lanes)
         self.lines = []
         # v[0 : 4NS) the tile being processed (A), v[4NS : 8NS) the next tile
-        # being loaded (B, software pipeline), then temporaries
-        self.B = 4 * self.NS
-        D = 8 * self.NS
+        # being loaded (B, software pipeline; dbuf only), then temporaries
+        self.B = 4 * self.NS if dbuf else 0
+        D = (8 if dbuf else 4) * self.NS
         self.D = D
-        self.T = [D + 0, D + 2, D + 4, D + 6]   # temporaries (double pairs)
-        self.C0, self.C1 = D + 8, D + 10
-        self.vLane, self.vLdB, self.vStB, self.vTmp = D + 12, D + 13, D + 14, D + 15
-        self.nvgpr = D + 16
+        # 16 temporaries (double pairs): pairs / elements of a handler cycle
+        # through 4 / 8 sets so that the scheduler can interleave them
+        self.T = [D + 2 * k for k in range(16)]
+        self.C0, self.C1 = D + 32, D + 34
+        self.vLane, self.vLdB, self.vStB, self.vTmp = D + 36, D + 37, D + 38, D + 39
+        self.nvgpr = D + 40      # 168 for R = 4: three waves per SIMD
         self.handlers = {}
+        self.buf = None          # straight-line region being collected for scheduling
 
     # ---- helpers --------------------------------------------------------
     def e(self, s):
-        self.lines.append("\t" + s)
+        if self.buf is not None:
+            self.buf.append(s)
+        else:
+            self.lines.append("\t" + s)
+
+    def region(self):
+        """Start collecting a straight-line VALU region (no DPP, no scalar
+        ops, no branches) to be list-scheduled by end_region()."""
+        self.buf = []
+
+    def end_region(self):
+        body, self.buf = self.buf, None
+        for ins in schedule(body):
+            self.lines.append("\t" + ins)
 
     def label(self, name):
         self.lines.append(name + ":")
@@ -124,6 +241,13 @@ class Gen:
         e("s_and_b64 s[96:97], s[32:33], s[72:73]")    # ctrlOut of the op
         e("s_cmp_eq_u64 s[96:97], s[72:73]")
         e("s_cbranch_scc0 .Lnext")
+        if self.W:
+            e("s_and_b32 s96, s3, s74")                 # wave bits that must be 1
+            e("s_cmp_eq_u32 s96, s74")
+            e("s_cbranch_scc0 .Lnext")
+            e("s_and_b32 s96, s3, s75")                 # wave bits that must be 0
+            e("s_cmp_eq_u32 s96, 0")
+            e("s_cbranch_scc0 .Lnext")
         e("s_add_u32 s98, s92, s68")                   # kernel base + handler offset
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
@@ -146,9 +270,9 @@ class Gen:
         self.e("s_mov_b64 exec, -1")
 
     # ---- pair math (in place, registers of j and f) ---------------------
-    def pair(self, kind, j, f):
+    def pair(self, kind, j, f, ts=0):
         r0, i0, r1, i1 = self.vp(self.re(j)), self.vp(self.im(j)), self.vp(self.re(f)), self.vp(self.im(f))
-        T = [self.vp(t) for t in self.T]
+        T = [self.vp(t) for t in self.T[4 * ts:4 * ts + 4]]
         m = self.sm
         e = self.e
         if kind == "M2":
@@ -212,18 +336,18 @@ class Gen:
         else:
             raise ValueError(kind)
 
-    def cmul_sgpr(self, j, kr, ki):
+    def cmul_sgpr(self, j, kr, ki, ts=0):
         # (x + iy) *= (m[kr] + i m[ki])
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
-        T = [self.vp(t) for t in self.T]
+        T = [self.vp(t) for t in self.T[2 * ts:2 * ts + 2]]
         self.e(f"v_mul_f64 {T[0]}, {self.sm(ki)}, {y}")
         self.e(f"v_mul_f64 {T[1]}, {self.sm(ki)}, {x}")
         self.e(f"v_fma_f64 {x}, {self.sm(kr)}, {x}, -{T[0]}")
         self.e(f"v_fma_f64 {y}, {self.sm(kr)}, {y}, {T[1]}")
 
-    def cmul_vgpr(self, j, cr, ci):
+    def cmul_vgpr(self, j, cr, ci, ts=0):
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
-        T = [self.vp(t) for t in self.T]
+        T = [self.vp(t) for t in self.T[2 * ts:2 * ts + 2]]
         self.e(f"v_mul_f64 {T[0]}, {self.vp(ci)}, {y}")
         self.e(f"v_mul_f64 {T[1]}, {self.vp(ci)}, {x}")
         self.e(f"v_fma_f64 {x}, {self.vp(cr)}, {x}, -{T[0]}")
@@ -234,9 +358,9 @@ class Gen:
         self.handler(idx_slot(kind, s, ctrl), f"{kind}_s{s}_c{ctrl}")
         if ctrl:
             self.ctrl_begin()
-        for j in range(self.NS):
-            if (j >> s) & 1:
-                continue
+        else:
+            self.region()
+        for p, j in enumerate([j for j in range(self.NS) if not (j >> s) & 1]):
             f = j | (1 << s)
             if ctrl:
                 skip = f".Lskip_{kind}_{s}_{j}"
@@ -244,15 +368,19 @@ class Gen:
                 self.pair(kind, j, f)
                 self.label(skip)
             else:
-                self.pair(kind, j, f)
+                self.pair(kind, j, f, p % 4)
         if ctrl:
             self.ctrl_end()
+        else:
+            self.end_region()
         self.back()
 
     def gen_d2s(self, s, ctrl):
         self.handler(idx_d2s(s, ctrl), f"D2S_s{s}_c{ctrl}")
         if ctrl:
             self.ctrl_begin()
+        else:
+            self.region()
         for j in range(self.NS):
             one = (j >> s) & 1
             if ctrl:
@@ -261,9 +389,11 @@ class Gen:
                 self.cmul_sgpr(j, 2 if one else 0, 3 if one else 1)
                 self.label(skip)
             else:
-                self.cmul_sgpr(j, 2 if one else 0, 3 if one else 1)
+                self.cmul_sgpr(j, 2 if one else 0, 3 if one else 1, j % 8)
         if ctrl:
             self.ctrl_end()
+        else:
+            self.end_region()
         self.back()
 
     def gen_d2l(self, ctrl):
@@ -271,7 +401,7 @@ class Gen:
         # per-lane coefficient: lane bit aux (s71) ? d1 : d0
         self.e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, s71, 1")
         self.e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
-        C0, C1, T0, T1 = self.C0, self.C1, self.T[0], self.T[1]
+        C0, C1, T0, T1 = self.C0, self.C1, self.T[14], self.T[15]
         self.e(f"v_mov_b64 {self.vp(C0)}, {self.sm(0)}")
         self.e(f"v_mov_b64 {self.vp(C1)}, {self.sm(1)}")
         self.e(f"v_mov_b64 {self.vp(T0)}, {self.sm(2)}")
@@ -281,6 +411,8 @@ class Gen:
             self.e(f"v_cndmask_b32_e32 v{c + 1}, v{c + 1}, v{t + 1}, vcc")
         if ctrl:
             self.ctrl_begin()
+        else:
+            self.region()
         for j in range(self.NS):
             if ctrl:
                 skip = f".Lskip_d2l_{j}"
@@ -288,9 +420,11 @@ class Gen:
                 self.cmul_vgpr(j, C0, C1)
                 self.label(skip)
             else:
-                self.cmul_vgpr(j, C0, C1)
+                self.cmul_vgpr(j, C0, C1, j % 7)
         if ctrl:
             self.ctrl_end()
+        else:
+            self.end_region()
         self.back()
 
     def gen_diag(self, creg, lane):
@@ -301,8 +435,10 @@ class Gen:
         e = self.e
         js = [j for j in range(self.NS) if (j & creg) == creg]
         if not lane:
-            for j in js:
-                self.cmul_sgpr(j, 0, 1)
+            self.region()
+            for k, j in enumerate(js):
+                self.cmul_sgpr(j, 0, 1, k % 8)
+            self.end_region()
             self.back()
             return
         C0, C1 = self.C0, self.C1
@@ -315,8 +451,10 @@ class Gen:
         e(f"v_cndmask_b32_e32 v{C0 + 1}, v{self.vTmp}, v{C0 + 1}, vcc")
         e(f"v_cndmask_b32_e32 v{C1}, 0, v{C1}, vcc")
         e(f"v_cndmask_b32_e32 v{C1 + 1}, 0, v{C1 + 1}, vcc")
-        for j in js:
-            self.cmul_vgpr(j, C0, C1)
+        self.region()
+        for k, j in enumerate(js):
+            self.cmul_vgpr(j, C0, C1, k % 8)
+        self.end_region()
         self.back()
 
     def gen_tr(self, s, l):
@@ -368,11 +506,49 @@ class Gen:
             # the next group's DPPs read other registers: no hazard
         self.back()
 
+    def gen_trw(self, s, b):
+        """Transpose slot s with wave bit b through LDS: the wave with the bit
+        clear sends its registers with slot bit s set and receives the
+        partner's registers with it clear (and vice versa), in place."""
+        self.handler(idx_trw(s, b), f"TRW_s{s}_b{b}")
+        e = self.e
+        vt, vl = self.vTmp, self.vLane
+        lo_regs, hi_regs = [], []
+        for j in range(self.NS):
+            if (j >> s) & 1:
+                continue
+            f = j | (1 << s)
+            lo_regs += [self.re(f), self.im(f)]
+            hi_regs += [self.re(j), self.im(j)]
+        ob = self.OUTBOX
+        e(f"s_mul_i32 s96, s3, {ob}")
+        e(f"v_lshlrev_b32_e32 v{vt}, 3, v{vl}")
+        e(f"v_add_u32_e32 v{vt}, s96, v{vt}")
+        for phase in ("w", "r"):
+            e(f"s_bitcmp1_b32 s3, {b}")
+            e(f"s_cbranch_scc1 .Ltrw_{s}_{b}_{phase}hi")
+            for regs, tag in ((lo_regs, "lo"), (hi_regs, "hi")):
+                if tag == "hi":
+                    self.label(f".Ltrw_{s}_{b}_{phase}hi")
+                for k, r in enumerate(regs):
+                    if phase == "w":
+                        e(f"ds_write_b64 v{vt}, v[{r}:{r + 1}] offset:{k * 512}")
+                    else:
+                        e(f"ds_read_b64 v[{r}:{r + 1}], v{vt} offset:{k * 512}")
+                if tag == "lo":
+                    e(f"s_branch .Ltrw_{s}_{b}_{phase}done")
+            self.label(f".Ltrw_{s}_{b}_{phase}done")
+            if phase == "w":
+                e(f"v_xor_b32_e32 v{vt}, {(1 << b) * ob}, v{vt}")   # the partner's outbox
+            e("s_waitcnt lgkmcnt(0)")
+            e("s_barrier")
+        self.back()
+
     # ---- the kernel -------------------------------------------------------
     def kernel(self):
         R, NS, D = self.R, self.NS, self.D
         NG = NS // 2       # 16-byte groups per array per lane
-        K = R + 6          # tile bits
+        K = R + 6 + self.W  # tile bits
         L = self.lines
         L.append('\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
         L.append("\t.amdhsa_code_object_version 6")
@@ -386,7 +562,15 @@ class Gen:
         vl, vldb, vstb, vt = self.vLane, self.vLdB, self.vStB, self.vTmp
         e("s_load_dwordx4 s[4:7], s[0:1], 0x0")       # re, im
         e("s_load_dwordx2 s[8:9], s[0:1], 0x10")      # launch record
-        e(f"v_and_b32_e32 v{vl}, 63, v0")     # one wave per workgroup
+        e(f"v_and_b32_e32 v{vl}, 63, v0")
+        if self.W:
+            # wave index in the workgroup (= its wave bits): lane 0's work-item id / 64
+            e("v_readfirstlane_b32 s3, v0")
+            e("s_nop 4")                          # VALU-written SGPR read by SALU / SMEM
+            e("s_lshr_b32 s3, s3, 6")
+            e(f"s_and_b32 s3, s3, {(1 << self.W) - 1}")
+        else:
+            e("s_mov_b32 s3, 0")
         e("s_getpc_b64 s[92:93]")
         self.label(".Lentry_pc")
         e("s_sub_u32 s92, s92, .Lentry_pc-qa_wave_tile")   # kernel base: handlers jump from here
@@ -405,27 +589,62 @@ class Gen:
         e("s_mov_b32 s16, s2")
         e("s_mov_b32 s17, 0")
         e("s_waitcnt vmcnt(0) lgkmcnt(0)")
-        # Software pipeline: while the ops run on tile i (registers A), tile
-        # i+1 is already loading into registers B; at the top of iteration
-        # i+1 B is copied to A.  Prologue: load the first tile into B.
-        self.tile_check("s[16:17]", ".Ldone")
-        self.base_of("s[16:17]", 68)
-        self.groups("ld", 88, vldb, NG, self.B, 70)
-        e("s_waitcnt vmcnt(0)")
-        e("s_branch .Lcopy")
-        self.label(".Ltile_loop")
-        e(f"s_waitcnt vmcnt({2 * NG})")   # tile i+1's loads are older than tile i's stores
-        self.label(".Lcopy")
-        for r in range(0, 4 * NS, 2):
-            e(f"v_mov_b64 v[{r}:{r + 1}], v[{self.B + r}:{self.B + r + 1}]")
-        self.base_of("s[16:17]", 32)     # this tile: ctrlOut tests and stores
-        # prefetch the next tile into B
-        e("s_add_u32 s72, s16, s14")
-        e("s_addc_u32 s73, s17, s15")
-        self.tile_check("s[72:73]", ".Lno_prefetch")
-        self.base_of("s[72:73]", 68)
-        self.groups("ld", 88, vldb, NG, self.B, 70)
-        self.label(".Lno_prefetch")
+        if self.dbuf:
+            # Software pipeline: while the ops run on tile i (registers A), tile
+            # i+1 is already loading into registers B; at the top of iteration
+            # i+1 B is copied to A.  Prologue: load the first tile into B.
+            self.tile_check("s[16:17]", ".Ldone")
+            self.base_of("s[16:17]", 68)
+            self.wave_bytes(856, 70)
+            if self.debug:
+                # debug: record (wave id, tile, base, load byte offset, lane 0's
+                # lane offset) per wave at launch+920 + 64 * (4 * wg + (s3 & 3))
+                # and stop before touching the state
+                e("s_load_dwordx2 s[94:95], s[8:9], 920")     # debug buffer
+                e("s_waitcnt lgkmcnt(0)")
+                e("s_and_b32 s98, s3, 3")
+                e("s_lshl_b32 s99, s2, 2")
+                e("s_add_u32 s98, s98, s99")
+                e("s_lshl_b32 s98, s98, 6")
+                e("s_add_u32 s94, s94, s98")
+                e("s_addc_u32 s95, s95, 0")
+                vals = ["s3", "s16", "s17", "s68", "s69", "s96", "s97", "s2"]
+                for k, sv in enumerate(vals):
+                    e(f"v_mov_b32_e32 v{self.T[0] + (k % 8)}, {sv}")
+                e(f"v_mov_b32_e32 v{self.T[4]}, 0")
+                e("s_nop 1")
+                e(f"v_cmp_eq_u32_e32 vcc, 0, v{vl}")
+                e("s_and_saveexec_b64 s[98:99], vcc")
+                e(f"global_store_dwordx4 v{self.T[4]}, v[{self.T[0]}:{self.T[0] + 3}], s[94:95]")
+                e(f"global_store_dwordx4 v{self.T[4]}, v[{self.T[0] + 4}:{self.T[0] + 7}], s[94:95] offset:16")
+                e(f"global_store_dword v{self.T[4]}, v{vldb}, s[94:95] offset:32")
+                e("s_waitcnt vmcnt(0)")
+                e("s_endpgm")
+            self.groups("ld", 88, vldb, NG, self.B, 96)
+            e("s_waitcnt vmcnt(0)")
+            e("s_branch .Lcopy")
+            self.label(".Ltile_loop")
+            e(f"s_waitcnt vmcnt({2 * NG})")   # tile i+1's loads are older than tile i's stores
+            self.label(".Lcopy")
+            for r in range(0, 4 * NS, 2):
+                e(f"v_mov_b64 v[{r}:{r + 1}], v[{self.B + r}:{self.B + r + 1}]")
+            self.base_of("s[16:17]", 32)     # this tile: ctrlOut tests and stores
+            # prefetch the next tile into B
+            e("s_add_u32 s72, s16, s14")
+            e("s_addc_u32 s73, s17, s15")
+            self.tile_check("s[72:73]", ".Lno_prefetch")
+            self.base_of("s[72:73]", 68)
+            self.wave_bytes(856, 70)
+            self.groups("ld", 88, vldb, NG, self.B, 96)
+            self.label(".Lno_prefetch")
+        else:
+            # one tile at a time (latency hidden by the other waves of the SIMD)
+            self.label(".Ltile_loop")
+            self.tile_check("s[16:17]", ".Ldone")
+            self.base_of("s[16:17]", 32)
+            self.wave_bytes(856, 34)
+            self.groups("ld", 88, vldb, NG, 0, 96)
+            e("s_waitcnt vmcnt(0)")
         # ---- op loop: prefetch op 0, then every op starts through next_op()
         e("s_mov_b32 s19, 0")
         e("s_mov_b64 s[94:95], s[10:11]")
@@ -435,10 +654,12 @@ class Gen:
         self.next_op()
         self.label(".Lops_done")
         e("s_waitcnt lgkmcnt(0)")      # the prefetch past the last op writes s[36:59]
-        self.groups("st", 216, vstb, NG, 0, 34)
+        self.wave_bytes(888, 34)
+        self.groups("st", 216, vstb, NG, 0, 96)
         e("s_add_u32 s16, s16, s14")
         e("s_addc_u32 s17, s17, s15")
-        self.tile_check("s[16:17]", ".Ldone")
+        if self.dbuf:
+            self.tile_check("s[16:17]", ".Ldone")
         e("s_branch .Ltile_loop")
         self.label(".Ldone")
         e("s_endpgm")
@@ -458,6 +679,9 @@ class Gen:
         for s in range(1, R):
             for l in range(6):
                 self.gen_tr(s, l)
+        for s in range(1, R):
+            for b in range(self.W):
+                self.gen_trw(s, b)
         L.append(".Lfunc_end0:")
         L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
         self.descriptor()
@@ -469,12 +693,27 @@ class Gen:
         self.e(f"s_subb_u32 s99, s{lo + 1}, s13")
         self.e(f"s_cbranch_scc0 {done}")
 
+    def wave_bytes(self, off, bpair):
+        """s[96:97] = s[bpair:bpair+1] + this wave's byte offset (launch record
+        + off + 8 * wave): the tile bits on wave bits are uniform per wave."""
+        e = self.e
+        if not self.W:
+            e(f"s_mov_b64 s[96:97], s[{bpair}:{bpair + 1}]")
+            return
+        e("s_lshl_b32 s98, s3, 3")
+        e(f"s_add_u32 s98, s98, {off}")
+        e("s_load_dwordx2 s[96:97], s[8:9], s98 offset:0x0")   # SGPR offset, SOE form
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"s_add_u32 s96, s96, s{bpair}")
+        e(f"s_addc_u32 s97, s97, s{bpair + 1}")
+
     def base_of(self, tile, d):
         """s[d:d+1] = tile index with zeros inserted at pos[0..K-1] (ascending),
         s[d+2:d+3] = the same in bytes."""
         e = self.e
         e(f"s_mov_b64 s[{d}:{d + 1}], {tile}")
-        for b in range(self.R + 6):
+        assert self.R + 6 + self.W <= 12, "pos[] lives in s[20:31]"
+        for b in range(self.R + 6 + self.W):
             p = f"s{20 + b}"
             e(f"s_bfm_b64 s[96:97], {p}, 0")
             e(f"s_and_b64 s[98:99], s[{d}:{d + 1}], s[96:97]")
@@ -521,7 +760,8 @@ class Gen:
         L.append("\t.section\t.rodata,\"a\",@progbits")
         L.append("\t.p2align\t6, 0x0")
         L.append("\t.amdhsa_kernel qa_wave_tile")
-        for k, v in [("group_segment_fixed_size", 0), ("private_segment_fixed_size", 0), ("kernarg_size", 24),
+        lds = self.NW * self.OUTBOX if self.W else 0
+        for k, v in [("group_segment_fixed_size", lds), ("private_segment_fixed_size", 0), ("kernarg_size", 24),
                      ("user_sgpr_count", 2), ("user_sgpr_dispatch_ptr", 0), ("user_sgpr_queue_ptr", 0),
                      ("user_sgpr_kernarg_segment_ptr", 1), ("user_sgpr_dispatch_id", 0),
                      ("user_sgpr_kernarg_preload_length", 0), ("user_sgpr_kernarg_preload_offset", 0),
@@ -555,14 +795,14 @@ amdhsa.kernels:
         .offset:         16
         .size:           8
         .value_kind:     global_buffer
-    .group_segment_fixed_size: 0
+    .group_segment_fixed_size: {lds}
     .kernarg_segment_align: 8
     .kernarg_segment_size: 24
     .language:       OpenCL C
     .language_version:
       - 2
       - 0
-    .max_flat_workgroup_size: 64
+    .max_flat_workgroup_size: {64 * self.NW}
     .name:           qa_wave_tile
     .private_segment_fixed_size: 0
     .sgpr_count:     102
@@ -609,12 +849,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("mode", choices=["asm", "embed"])
     ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--dbuf", type=int, default=-1, help="software-pipelined tiles (default: when 4 slots)")
+    ap.add_argument("--wbits", type=int, default=2, help="2^wbits waves share a tile")
+    ap.add_argument("--debug", action="store_true", help="record addressing state per wave and stop (no state access)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--obj")
     ap.add_argument("--hsaco")
     args = ap.parse_args()
     if args.mode == "asm":
-        g = Gen(args.slots)
+        g = Gen(args.slots, args.dbuf if args.dbuf >= 0 else args.slots <= 4, args.wbits, args.debug)
         g.kernel()
         with open(args.out, "w") as f:
             f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
@@ -634,6 +877,7 @@ def main():
     with open(args.out, "w") as f:
         f.write("// GENERATED by tools/gen_wave_asm.py embed -- do not edit\n")
         f.write(f"static const int kWaveImageSlots = {args.slots};\n")
+        f.write(f"static const int kWaveImageWBits = {args.wbits};\n")
         f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
         f.write(f"static const unsigned char kWaveImage[{len(img)}] __attribute__((aligned(4096))) = {{\n")
         for k in range(0, len(img), 24):

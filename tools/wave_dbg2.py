@@ -1,0 +1,10 @@
+import os, sys
+sys.path.insert(0, "/root/repo")
+import quest_amd as qa
+from quest_amd.ops import capi
+env = qa.Env()
+reg = qa.Register(env, 18)
+reg.init_plus()
+for q in range(18): reg.z(q)
+reg.sync()
+print("ok")
