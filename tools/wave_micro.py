@@ -47,12 +47,20 @@ def main():
         "CNOT lane->slot": lambda: [reg.cnot(lane_q[i % 6], slot_q[i % 4]) for i in range(c)],
         "H lanes 1-3 (TR l0-2)": lambda: [reg.h(1 + i % 3) for i in range(c)],
         "H lanes 7-9 (TR l3-5)": lambda: [reg.h(7 + i % 3) for i in range(c)],
+        # 12 distinct qubits in one pass: some sit on wave bits (TRW through LDS)
+        "H 12 qubits (TRW)": lambda: [(reg.h(i % 12), reg.cz(i % 12, (i + 1) % 12)) for i in range(c)],
+        "H 10 qubits (no TRW)": lambda: [(reg.h(i % 10), reg.cz(i % 10, (i + 1) % 10)) for i in range(c)],
         # compute-bound: many ops in one pass (CZ breaks one-qubit fusion)
         "heavy M2 x200": lambda: [(reg.unitary(0, [[0.6, 0.8j], [0.8j, 0.6]]), reg.unitary(4, [[0.6, 0.8j], [0.8j, 0.6]]),
                                    reg.cz(0, 4)) for i in range(100)],
         "heavy M2R x200": lambda: [(reg.h(0), reg.h(4), reg.cz(0, 4)) for i in range(100)],
         "heavy DIAG x240": lambda: [reg.t(i % 4) for i in range(240)],
         "heavy TRl5 x120": lambda: [(reg.h(9), reg.h(8), reg.cz(8, 9)) for i in range(80)],
+        # op lists that fit the scalar cache (~9 KB of records)
+        "mid M2 x96": lambda: [(reg.unitary(0, [[0.6, 0.8j], [0.8j, 0.6]]), reg.unitary(4, [[0.6, 0.8j], [0.8j, 0.6]]),
+                                reg.cz(0, 4)) for i in range(48)],
+        "mid M2R x96": lambda: [(reg.h(0), reg.h(4), reg.cz(0, 4)) for i in range(48)],
+        "mid DIAG x96": lambda: [reg.t(i % 4) for i in range(96)],
     }
     res = {}
     for r in range(args.reps):
