@@ -83,6 +83,8 @@ typedef struct QuESTStats {
     long long wavePasses;     /* passes run by the register-resident wave-tile engine */
     long long waveOps;        /* ops of those passes, including transpositions */
     long long waveTransposes; /* cross-lane transpositions among them */
+    long long relabels;       /* X/Y-like gates on rank qubits applied by relabelling chunks (no data moved) */
+    long long globalDiags;    /* diagonal one-qubit gates on rank qubits applied as per-rank scalings */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

@@ -80,7 +80,8 @@ class _Binding:
         class QuESTStats(C.Structure):
             _fields_ = [(n, C.c_longlong) for n in
                         ("opsQueued", "passes", "fusedOps", "swaps", "bytesExchanged", "reductions",
-                         "verifiedFlushes", "wavePasses", "waveOps", "waveTransposes")]
+                         "verifiedFlushes", "wavePasses", "waveOps", "waveTransposes", "relabels",
+                         "globalDiags")]
 
         self.Complex, self.ComplexMatrix2, self.Vector = Complex, ComplexMatrix2, Vector
         self.ComplexArray, self.QASMLogger, self.Qureg = ComplexArray, QASMLogger, Qureg

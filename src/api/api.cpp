@@ -838,6 +838,7 @@ void initStateFromSingleFile(Qureg* qureg, char filename[200], QuESTEnv env) {
     QuregImpl& q = Q(*qureg);
     FILE* fp = fopen(filename, "r");
     if (!v::fileOpened(fp != nullptr, __func__)) return;
+    router::prepareOverwrite(q);  // rank r reads the lines of chunk r
     std::vector<real> re((size_t)q.numAmpsPerChunk, 0), im(re.size(), 0);
     char line[200];
     i64 total = 0, mine = 0;
@@ -967,6 +968,8 @@ void getQuESTStats(QuESTStats* s) {
     s->wavePasses = stats().wavePasses;
     s->waveOps = stats().waveOps;
     s->waveTransposes = stats().waveTransposes;
+    s->relabels = stats().relabels;
+    s->globalDiags = stats().globalDiags;
 }
 
 void resetQuESTStats(void) { stats() = Stats(); }

@@ -64,8 +64,11 @@ struct QuregImpl {
     int L;               // physical qubits held locally (nSV - log2 numChunks)
     i64 numAmpsPerChunk;
     i64 numAmpsTotal;
-    int chunkId;
+    int chunkId;         // LOGICAL chunk held by this rank (rank qubits' values)
     int numChunks;
+    // logical chunk -> rank holding it.  Identity unless an X-like gate on a
+    // rank qubit relabelled chunks instead of moving their data (router).
+    std::vector<int> chunkRank;
     real* re;            // this chunk's amplitudes (device memory on the HIP build)
     real* im;
     int l2p[64];         // logical qubit -> physical bit position

@@ -68,6 +68,41 @@ inline int chunkBit(const QuregImpl& q, int phys) { return (q.chunkId >> (phys -
 
 inline bool distributed(const QuregImpl& q) { return q.L < q.nSV; }
 
+// Rank holding logical chunk c (see QuregImpl::chunkRank).
+inline int rankOf(const QuregImpl& q, int c) { return q.chunkRank.empty() ? c : q.chunkRank[(size_t)c]; }
+
+void resetChunks(QuregImpl& q) {
+    q.chunkId = rt().rank;
+    q.chunkRank.resize((size_t)q.numChunks);
+    for (int c = 0; c < q.numChunks; c++) q.chunkRank[(size_t)c] = c;
+}
+
+bool chunksIdentity(const QuregImpl& q) {
+    for (int c = 0; c < (int)q.chunkRank.size(); c++)
+        if (q.chunkRank[(size_t)c] != c) return false;
+    return true;
+}
+
+inline bool isZero(cplx a) { return a.re == 0 && a.im == 0; }
+inline bool isOne(cplx a) { return a.re == 1 && a.im == 0; }
+
+// How a logical op can run given the set of local logical qubits.  A
+// one-qubit gate on a RANK qubit needs no data movement when its matrix is
+// diagonal (each rank scales its chunk by m[b][b], b = its rank bit) or
+// anti-diagonal with only rank-qubit controls (X, Y, controlled-X between
+// rank qubits: the chunks trade labels, then each scales by m[b][1-b]).
+// The reference exchanges half chunks for every such gate
+// (QuEST_cpu_distributed.c:1009-1115, statevec_pauliXDistributed / pauliY).
+enum class Place { Local, RankDiag, RankAnti, Blocked };
+
+Place placement(const Op& op, u64 tg, u64 local) {
+    if (!(tg & ~local)) return Place::Local;
+    if (op.kind != OpKind::Mat2 || op.nt != 1) return Place::Blocked;
+    if (isZero(op.m[1]) && isZero(op.m[2])) return Place::RankDiag;
+    if (isZero(op.m[0]) && isZero(op.m[3]) && !(op.ctrl & local)) return Place::RankAnti;
+    return Place::Blocked;
+}
+
 void enqueue(QuregImpl& q, const Op& op) {
     be::enqueue(q, op);
     stats().opsQueued++;
@@ -116,11 +151,13 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         const i64 n = std::min(slice, partSize - off);
         for (int d = 1; d < parts; d++) {
             const int j = myG ^ d;
-            int peer = q.chunkId;
+            // peers are paired by logical chunk (step d matches chunk c with
+            // c ^ D(d) on every rank), then mapped to the rank holding it
+            int peerChunk = q.chunkId;
             for (int m = 0; m < k; m++)
-                if ((d >> m) & 1) peer ^= 1 << (gpos[m] - q.L);
+                if ((d >> m) & 1) peerChunk ^= 1 << (gpos[m] - q.L);
             be::packBits(q, lpos, k, setMask[j], off, n, g_x.send[d - 1], g_x.send[d - 1] + n);
-            xs[d - 1] = {peer, g_x.send[d - 1], g_x.recv[d - 1], sizeof(real) * 2 * (size_t)n};
+            xs[d - 1] = {rankOf(q, peerChunk), g_x.send[d - 1], g_x.recv[d - 1], sizeof(real) * 2 * (size_t)n};
         }
         comm::exchange(xs.data(), parts - 1);
         for (int d = 1; d < parts; d++) {
@@ -166,6 +203,81 @@ void issue(QuregImpl& q, const Op& lop) {
         }
     }
     enqueue(q, op);
+}
+
+// Per-rank scalar (times a local-control mask): Diag op over the chunk.
+void scaleChunk(QuregImpl& q, u64 localCtrl, cplx s) {
+    if (isOne(s)) return;
+    Op op;
+    op.kind = OpKind::Diag;
+    op.nt = 0;
+    op.ctrl = localCtrl;
+    op.m[0] = s;
+    enqueue(q, op);
+}
+
+// Diagonal one-qubit gate on a rank qubit: scale by m[b][b].
+void issueRankDiag(QuregImpl& q, const Op& lop) {
+    const int b = chunkBit(q, q.l2p[lop.t[0]]);
+    u64 ctrl = 0;
+    for (u64 c = lop.ctrl; c; c &= c - 1) {
+        const int p = q.l2p[__builtin_ctzll(c)];
+        if (p >= q.L) {
+            if (!chunkBit(q, p)) return;
+        } else {
+            ctrl |= 1ull << p;
+        }
+    }
+    stats().globalDiags++;
+    scaleChunk(q, ctrl, lop.m[b ? 3 : 0]);
+}
+
+// Anti-diagonal one-qubit gate on a rank qubit, controls on rank qubits
+// only: every chunk satisfying the controls trades its label with the chunk
+// differing in the target bit (the same table update on every rank), then the
+// new amplitude at bit b is m[b][1-b] times the old one at 1-b.
+void issueRankAnti(QuregImpl& q, const Op& lop) {
+    const int tb = 1 << (q.l2p[lop.t[0]] - q.L);
+    int cm = 0;
+    for (u64 c = lop.ctrl; c; c &= c - 1) cm |= 1 << (q.l2p[__builtin_ctzll(c)] - q.L);
+    std::vector<int> nr(q.chunkRank);
+    for (int c = 0; c < q.numChunks; c++)
+        if ((c & cm) == cm) nr[(size_t)(c ^ tb)] = q.chunkRank[(size_t)c];
+    q.chunkRank.swap(nr);
+    stats().relabels++;
+    if ((q.chunkId & cm) != cm) return;
+    q.chunkId ^= tb;
+    const int b = (q.chunkId & tb) ? 1 : 0;
+    scaleChunk(q, 0, lop.m[b ? 2 : 1]);
+}
+
+// Move the data so that rank r holds logical chunk r again: pairwise
+// whole-chunk exchanges, the same sequence on every rank.
+void restoreChunks(QuregImpl& q) {
+    if (chunksIdentity(q)) return;
+    be::flush(q);
+    const i64 slice = std::min<i64>(q.numAmpsPerChunk, std::max<i64>(rt().exchangeSliceBytes / (i64)(2 * sizeof(real)), 1));
+    ensureXBuf(1, slice);
+    const int me = rt().rank;
+    for (int r = 0; r < q.numChunks; r++) {
+        const int s = q.chunkRank[(size_t)r];  // rank holding chunk r
+        if (s == r) continue;
+        int x = 0;  // chunk held by rank r
+        while (q.chunkRank[(size_t)x] != r) x++;
+        if (me == r || me == s) {
+            const int peer = me == r ? s : r;
+            for (i64 off = 0; off < q.numAmpsPerChunk; off += slice) {
+                const i64 n = std::min(slice, q.numAmpsPerChunk - off);
+                be::toBuffer(q, off, n, g_x.send[0], g_x.send[0] + n);
+                comm::sendrecv(peer, g_x.send[0], g_x.recv[0], sizeof(real) * 2 * (size_t)n);
+                be::fromBuffer(q, off, n, g_x.recv[0], g_x.recv[0] + n);
+                stats().bytesExchanged += (long long)(sizeof(real) * 2 * n);
+            }
+            q.chunkId = me == r ? r : x;
+        }
+        q.chunkRank[(size_t)r] = r;
+        q.chunkRank[(size_t)x] = s;
+    }
 }
 
 // Choose the qubits to bring onto local positions for the queued ops (the
@@ -217,8 +329,14 @@ void flushLogical(QuregImpl& q) {
         u64 blockedTg = 0, blockedTouch = 0;
         for (const Op& op : lq) {
             const u64 tg = logicalTargets(op), touch = tg | op.ctrl;
-            if (!(tg & blockedTouch) && !(touch & blockedTg) && !(tg & ~local)) {
-                issue(q, op);
+            const Place pl = placement(op, tg, local);
+            if (!(tg & blockedTouch) && !(touch & blockedTg) && pl != Place::Blocked) {
+                if (pl == Place::Local)
+                    issue(q, op);
+                else if (pl == Place::RankDiag)
+                    issueRankDiag(q, op);
+                else
+                    issueRankAnti(q, op);
             } else {
                 rest.push_back(op);
                 blockedTg |= tg;
@@ -248,11 +366,13 @@ void drain(QuregImpl& q) {
     be::flush(q);
 }
 
+// Identity qubit layout and chunk placement (callers overwrite the state).
 void resetLayout(QuregImpl& q) {
     for (int i = 0; i < 64; i++) {
         q.l2p[i] = q.p2l[i] = i;
         q.lastUse[i] = 0;
     }
+    resetChunks(q);
 }
 
 i64 logicalToPhysicalIndex(const QuregImpl& q, i64 idx) {
@@ -273,7 +393,6 @@ void create(QuregImpl& q, int nSV, bool density) {
     q.nRep = density ? nSV / 2 : nSV;
     q.L = nSV - g;
     q.numChunks = rt().numRanks;
-    q.chunkId = rt().rank;
     q.numAmpsTotal = (i64)1 << nSV;
     q.numAmpsPerChunk = (i64)1 << q.L;
     resetLayout(q);
@@ -467,6 +586,8 @@ void clone(QuregImpl& dst, QuregImpl& src) {
     memcpy(dst.l2p, src.l2p, sizeof dst.l2p);
     memcpy(dst.p2l, src.p2l, sizeof dst.p2l);
     memcpy(dst.lastUse, src.lastUse, sizeof dst.lastUse);
+    dst.chunkId = src.chunkId;  // each rank copied its own (logical) chunk
+    dst.chunkRank = src.chunkRank;
     dst.useClock = src.useClock;
 }
 
@@ -501,7 +622,7 @@ void densInitPure(QuregImpl& rho, QuregImpl& psi) {
 void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
     drain(a);  // routing may move qubits: compare layouts afterwards
     drain(b);
-    if (memcmp(a.l2p, b.l2p, sizeof(int) * a.nSV) != 0) {
+    if (memcmp(a.l2p, b.l2p, sizeof(int) * a.nSV) != 0 || a.chunkRank != b.chunkRank) {
         canonicalise(a);
         canonicalise(b);
     }
@@ -510,7 +631,7 @@ void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
 
 void canonicalise(QuregImpl& q) {
     drain(q);
-    if (q.permIdentity()) return;
+    if (q.permIdentity() && chunksIdentity(q)) return;
     // 1. the right logical qubit on every global position, in all-to-all
     //    rounds: first every global position whose qubit is local comes in;
     //    qubits stuck on the wrong global position are first moved out to
@@ -540,7 +661,9 @@ void canonicalise(QuregImpl& q) {
         if (k == 0) break;
         multiSwap(q, gp, lp, k);
     }
-    // 2. permute local qubits with local SWAP ops
+    // 2. every rank holds its own chunk again (undo X-gate relabellings)
+    restoreChunks(q);
+    // 3. permute local qubits with local SWAP ops
     static const cplx kSwap[16] = {{1, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 0}, {0, 0},
                                    {0, 0}, {1, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 0}};
     for (int i = 0; i < q.L; i++) {
@@ -572,7 +695,7 @@ cplx getAmp(QuregImpl& q, i64 flatIndex) {
     int owner = (int)(p >> q.L);
     real v[2] = {0, 0};
     if (owner == q.chunkId) be::readAmps(q, p & (q.numAmpsPerChunk - 1), &v[0], &v[1], 1);
-    if (q.numChunks > 1) comm::bcastHost(v, sizeof v, owner);
+    if (q.numChunks > 1) comm::bcastHost(v, sizeof v, rankOf(q, owner));
     return {v[0], v[1]};
 }
 
@@ -614,7 +737,7 @@ double densTrace(QuregImpl& q) { return densDiag(q, -1); }
 cplx inner(QuregImpl& bra, QuregImpl& ket) {
     drain(bra);  // routing may move qubits: compare layouts afterwards
     drain(ket);
-    if (memcmp(bra.l2p, ket.l2p, sizeof(int) * bra.nSV) != 0) {
+    if (memcmp(bra.l2p, ket.l2p, sizeof(int) * bra.nSV) != 0 || bra.chunkRank != ket.chunkRank) {
         canonicalise(bra);
         canonicalise(ket);
     }

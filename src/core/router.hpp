@@ -73,6 +73,8 @@ struct Stats {
     long long verifiedFlushes = 0;
     long long wavePasses = 0;     // passes run by the wave-tile engine
     long long waveOps = 0, waveTransposes = 0;  // their ops / cross-lane transpositions
+    long long relabels = 0;       // anti-diagonal gates on rank qubits done by relabelling chunks
+    long long globalDiags = 0;    // diagonal gates on rank qubits done as per-rank scalings
 };
 Stats& stats();
 

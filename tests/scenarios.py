@@ -127,8 +127,76 @@ def qasm_log(env):
     return {"qasm": text}
 
 
+def rank_qubit_gates(env):
+    """X/Y-like and diagonal gates on the top (rank) qubits, mixed with gates
+    that do need a swap, then every read that depends on which rank holds
+    which chunk: getAmp, probabilities, inner product with a register laid
+    out differently, clone, measurement, a checkpoint round trip and the
+    full state.  On >1 rank the anti-diagonal gates relabel chunks instead of
+    moving data (the ``_relabels`` key, absent on one rank)."""
+    import os
+    import tempfile
+
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    n = 8
+    r = qa.Register(env, n)
+    r.init_plus()
+    random_layered(n, 2, seed=5).apply(r)
+    capi.canonicaliseQureg(r.q)   # logical qubits n-1.. on the rank bits
+    capi.resetQuESTStats()
+    for k in range(3):
+        r.x(7)                # anti-diagonal on a rank qubit: relabel
+        r.rz(7, 0.3 + k)      # diagonal on a rank qubit: per-rank scaling
+        r.unitary(7, [[0, 0.6 + 0.8j], [1j, 0]])
+        r.y(6)
+        r.cnot(7, 6)
+        r.t(6)
+        r.z(7)
+        r.s(6)
+        r.phase(7, 0.2)
+        r.x(6)
+        r.cy(6, 7)            # rank control and target on 4 ranks
+        r.h(2)
+        r.cnot(1, 7)          # local control, rank target: needs data
+        r.ry(5, 0.2)
+    r.sync()
+    st = capi.getQuESTStats()
+    out = {"amps": np.array([r.amp(i) for i in (0, 5, 77, 200, 255)]),
+           "probs": np.array([r.prob(q, 1) for q in range(n)])}
+    b = qa.Register(env, n)
+    b.init_plus()
+    b.rx(7, 0.4)
+    out["inner"] = r.inner(b)
+    c = qa.Register(env, n)
+    c.clone_from(r)
+    c.x(7)
+    c.h(0)
+    out["clone_state"] = c.to_numpy()
+    out["clone_inner"] = c.inner(r)
+    r.x(6)
+    # the ranks of one run are siblings: the parent's pid names a shared path
+    path = os.path.join(tempfile.gettempdir(), f"qa_relabel_{env.num_ranks}_{os.getppid()}_{os.getpid() if env.num_ranks == 1 else 0}")
+    assert r.save(path)
+    r.x(7)
+    assert r.load(path)
+    out["state"] = r.to_numpy()
+    capi.seedQuEST([5, 6], 2)
+    r.x(7)
+    out["outcomes"] = np.array([r.measure(q) for q in (7, 6, 0)])
+    out["after"] = r.to_numpy()
+    if env.num_ranks > 1:
+        out["_relabels"] = st["relabels"]
+        out["_global_diags"] = st["globalDiags"]
+    for x in (r, b, c):
+        x.close()
+    return out
+
+
 SCENARIOS = {f.__name__: f for f in (random_ops_statevector, random_ops_density, measurement_and_collapse,
-                                     calculations, qasm_log)}
+                                     calculations, qasm_log, rank_qubit_gates)}
 
 
 def checkpoint_save(env):

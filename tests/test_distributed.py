@@ -47,3 +47,16 @@ def test_distributed_equivalence(env, tmp_path, name, ranks):
             assert str(g) == v, k
         else:
             np.testing.assert_allclose(np.asarray(g), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_rank_qubit_relabels(env, tmp_path, ranks):
+    """X/Y/CNOT among rank qubits relabel chunks (no data moved) and diagonal
+    gates on rank qubits scale per rank; reads, clone, inner products,
+    checkpoints and measurement still see the logical state."""
+    want = _single("rank_qubit_gates", env)
+    got = _multi("rank_qubit_gates", ranks, tmp_path)
+    for k, v in want.items():
+        np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+    assert int(got["_relabels"]) > 0
+    assert int(got["_global_diags"]) > 0
