@@ -173,6 +173,10 @@ void readEnvConfig() {
         long long mb = atoll(s);
         if (mb > 0) rt().exchangeSliceBytes = mb << 20;
     }
+    if (const char* s = getenv("QUEST_EXCHANGE_SLICE_KB")) {  // tests: many slices on small registers
+        long long kb = atoll(s);
+        if (kb > 0) rt().exchangeSliceBytes = kb << 10;
+    }
 }
 
 }  // namespace

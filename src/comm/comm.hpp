@@ -42,6 +42,13 @@ struct Xfer {
     size_t bytes;
 };
 void exchange(const Xfer* x, int n);
+// Pipelined form: the exchange is ordered after everything already queued on
+// the compute stream but runs on a communication stream of its own, so the
+// compute stream can pack / unpack other slices meanwhile; exchangeWait(slot)
+// orders later compute-stream work after the exchange issued with that slot
+// (0 or 1).  Stream-less transports finish inside exchangeAsync.
+void exchangeAsync(const Xfer* x, int n, int slot);
+void exchangeWait(int slot);
 // In-place sum of host doubles across ranks.
 void allreduceSum(double* vals, int n);
 // In-place logical AND of a host int across ranks.

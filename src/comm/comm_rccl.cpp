@@ -58,6 +58,9 @@ bool g_socket = false;          // QUEST_COMM=socket test transport
 char* g_stage = nullptr;        // pinned staging for the socket transport
 size_t g_stageBytes = 0;
 ncclComm_t g_comm = nullptr;
+// communication stream of the pipelined exchange and its events
+hipStream_t g_cstream = nullptr;
+hipEvent_t g_ready = nullptr, g_done[2] = {nullptr, nullptr};
 double* g_dScalars = nullptr;   // device scratch for scalar collectives
 double* g_hScalars = nullptr;   // pinned host mirror
 std::string g_libName;
@@ -209,6 +212,9 @@ void init(int rank, int size) {
     }
     QA_HIP_CHECK(hipMalloc(&g_dScalars, sizeof(double) * 64));
     QA_HIP_CHECK(hipHostMalloc(&g_hScalars, sizeof(double) * 64, hipHostMallocDefault));
+    QA_HIP_CHECK(hipStreamCreateWithFlags(&g_cstream, hipStreamNonBlocking));
+    QA_HIP_CHECK(hipEventCreateWithFlags(&g_ready, hipEventDisableTiming));
+    for (hipEvent_t& e : g_done) QA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipk::setSyncWatchdog(watchdog);
 }
 
@@ -225,6 +231,13 @@ void finalize() {
         hipk::setSyncWatchdog(nullptr);
         R.commDestroy(g_comm);
         g_comm = nullptr;
+        if (g_cstream) {
+            (void)hipStreamSynchronize(g_cstream);
+            (void)hipEventDestroy(g_ready);
+            for (hipEvent_t e : g_done) (void)hipEventDestroy(e);
+            (void)hipStreamDestroy(g_cstream);
+            g_cstream = nullptr;
+        }
         (void)hipFree(g_dScalars);
         (void)hipHostFree(g_hScalars);
         g_dScalars = g_hScalars = nullptr;
@@ -266,6 +279,32 @@ void exchange(const Xfer* x, int n) {
         QA_NCCL(R.recv(x[i].recv, x[i].bytes, ncclUint8, x[i].peer, g_comm, S()), "ncclRecv");
     }
     QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+}
+
+bool pipelined() {
+    static const bool off = getenv("QUEST_EXCHANGE_PIPELINE") && atoi(getenv("QUEST_EXCHANGE_PIPELINE")) == 0;
+    return !off && !g_socket && g_size > 1 && g_cstream;
+}
+
+void exchangeAsync(const Xfer* x, int n, int slot) {
+    if (!pipelined()) {
+        exchange(x, n);
+        return;
+    }
+    QA_HIP_CHECK(hipEventRecord(g_ready, S()));
+    QA_HIP_CHECK(hipStreamWaitEvent(g_cstream, g_ready, 0));
+    QA_NCCL(R.groupStart(), "ncclGroupStart");
+    for (int i = 0; i < n; i++) {
+        QA_NCCL(R.send(x[i].send, x[i].bytes, ncclUint8, x[i].peer, g_comm, g_cstream), "ncclSend");
+        QA_NCCL(R.recv(x[i].recv, x[i].bytes, ncclUint8, x[i].peer, g_comm, g_cstream), "ncclRecv");
+    }
+    QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+    QA_HIP_CHECK(hipEventRecord(g_done[slot & 1], g_cstream));
+}
+
+void exchangeWait(int slot) {
+    if (!pipelined()) return;
+    QA_HIP_CHECK(hipStreamWaitEvent(S(), g_done[slot & 1], 0));
 }
 
 void allreduceSum(double* vals, int n) {

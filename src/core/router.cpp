@@ -53,6 +53,7 @@ struct XBuf {
 
 void ensureXBuf(int peers, i64 amps) {
     if ((int)g_x.send.size() >= peers && g_x.amps >= amps) return;
+    be::deviceSync();  // the communication stream may still read the old buffers
     for (real* p : g_x.send) be::freeComm(p);
     for (real* p : g_x.recv) be::freeComm(p);
     g_x.send.assign(peers, nullptr);
@@ -95,12 +96,25 @@ inline bool isOne(cplx a) { return a.re == 1 && a.im == 0; }
 // (QuEST_cpu_distributed.c:1009-1115, statevec_pauliXDistributed / pauliY).
 enum class Place { Local, RankDiag, RankAnti, Blocked };
 
+bool rankGatesOn() {
+    static const bool off = getenv("QUEST_RANK_GATES") && atoi(getenv("QUEST_RANK_GATES")) == 0;
+    return !off;
+}
+
 Place placement(const Op& op, u64 tg, u64 local) {
     if (!(tg & ~local)) return Place::Local;
-    if (op.kind != OpKind::Mat2 || op.nt != 1) return Place::Blocked;
+    if (!rankGatesOn() || op.kind != OpKind::Mat2 || op.nt != 1) return Place::Blocked;
     if (isZero(op.m[1]) && isZero(op.m[2])) return Place::RankDiag;
     if (isZero(op.m[0]) && isZero(op.m[3]) && !(op.ctrl & local)) return Place::RankAnti;
     return Place::Blocked;
+}
+
+// Whether the op's targets must be local wherever its controls sit (the swap
+// planner only counts such uses).
+bool targetsNeedLocal(const Op& op) {
+    if (!rankGatesOn() || op.kind != OpKind::Mat2 || op.nt != 1) return true;
+    if (isZero(op.m[1]) && isZero(op.m[2])) return false;
+    return !(isZero(op.m[0]) && isZero(op.m[3]) && op.ctrl == 0);
 }
 
 void enqueue(QuregImpl& q, const Op& op) {
@@ -136,10 +150,13 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     const int parts = 1 << k;
     const i64 partSize = q.numAmpsPerChunk >> k;
     i64 slice = (rt().exchangeSliceBytes >> (k - 1)) / (i64)(2 * sizeof(real));
-    slice = std::max<i64>(slice, ((i64)16 << 20) / (i64)(2 * sizeof(real)));
+    slice = std::max<i64>(slice, 16);
     slice = std::min(slice, partSize);
-    ensureXBuf(parts - 1, slice);
-    std::vector<comm::Xfer> xs(parts - 1);
+    // two buffer sets: slice s is packed into set s & 1 and exchanged on the
+    // communication stream while slice s - 1 is unpacked and s + 1 packed
+    const int np = parts - 1;
+    ensureXBuf(2 * np, slice);
+    std::vector<comm::Xfer> xs[2] = {std::vector<comm::Xfer>(np), std::vector<comm::Xfer>(np)};
     std::vector<u64> setMask(parts);
     for (int j = 0; j < parts; j++) {
         u64 msk = 0;
@@ -147,25 +164,38 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
             if ((j >> m) & 1) msk |= 1ull << lpos[m];
         setMask[j] = msk;
     }
-    for (i64 off = 0; off < partSize; off += slice) {
-        const i64 n = std::min(slice, partSize - off);
+    const i64 nSlices = (partSize + slice - 1) / slice;
+    auto unpack = [&](i64 s) {
+        const int b = (int)(s & 1);
+        const i64 off = s * slice, n = std::min(slice, partSize - off);
         for (int d = 1; d < parts; d++) {
-            const int j = myG ^ d;
+            real* r = g_x.recv[(size_t)(b * np + d - 1)];
+            be::unpackBits(q, lpos, k, setMask[myG ^ d], off, n, r, r + n);
+        }
+    };
+    for (i64 s = 0; s < nSlices; s++) {
+        const int b = (int)(s & 1);
+        const i64 off = s * slice, n = std::min(slice, partSize - off);
+        for (int d = 1; d < parts; d++) {
             // peers are paired by logical chunk (step d matches chunk c with
             // c ^ D(d) on every rank), then mapped to the rank holding it
             int peerChunk = q.chunkId;
             for (int m = 0; m < k; m++)
                 if ((d >> m) & 1) peerChunk ^= 1 << (gpos[m] - q.L);
-            be::packBits(q, lpos, k, setMask[j], off, n, g_x.send[d - 1], g_x.send[d - 1] + n);
-            xs[d - 1] = {rankOf(q, peerChunk), g_x.send[d - 1], g_x.recv[d - 1], sizeof(real) * 2 * (size_t)n};
+            real* sb = g_x.send[(size_t)(b * np + d - 1)];
+            be::packBits(q, lpos, k, setMask[myG ^ d], off, n, sb, sb + n);
+            xs[b][(size_t)(d - 1)] = {rankOf(q, peerChunk), sb, g_x.recv[(size_t)(b * np + d - 1)],
+                                      sizeof(real) * 2 * (size_t)n};
         }
-        comm::exchange(xs.data(), parts - 1);
-        for (int d = 1; d < parts; d++) {
-            const int j = myG ^ d;
-            be::unpackBits(q, lpos, k, setMask[j], off, n, g_x.recv[d - 1], g_x.recv[d - 1] + n);
+        comm::exchangeAsync(xs[b].data(), np, b);
+        if (s > 0) {
+            comm::exchangeWait(1 - b);
+            unpack(s - 1);
         }
-        stats().bytesExchanged += (long long)(sizeof(real) * 2 * n) * (parts - 1);
+        stats().bytesExchanged += (long long)(sizeof(real) * 2 * n) * np;
     }
+    comm::exchangeWait((int)((nSlices - 1) & 1));
+    unpack(nSlices - 1);
     for (int m = 0; m < k; m++) {
         const int g = gpos[m], l = lpos[m];
         const int lg = q.p2l[g], ll = q.p2l[l];
@@ -289,13 +319,20 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
     const int INF = 1 << 30;
     int first[64];
     for (int i = 0; i < 64; i++) first[i] = INF;
-    for (int i = 0; i < (int)lq.size(); i++)
+    for (int i = 0; i < (int)lq.size(); i++) {
+        if (i > 0 && !targetsNeedLocal(lq[i])) continue;
         for (int t = 0; t < lq[i].nt; t++)
             if (first[lq[i].t[t]] == INF) first[lq[i].t[t]] = i;
+    }
     const u64 need0 = logicalTargets(lq[0]);
+    // On a fully connected xGMI node an all-to-all moving k qubits sends
+    // chunk / 2^k over each of 2^k - 1 links at once, so its time FALLS with
+    // k: every rank qubit is swapped whenever one must be, qubits nothing
+    // needs filling the spare positions (a k = 1 swap would push half the
+    // chunk through a single link).
     std::vector<int> in, out;
     for (int lg = 0; lg < q.nSV; lg++)
-        if (q.l2p[lg] >= q.L && first[lg] < INF) in.push_back(lg);
+        if (q.l2p[lg] >= q.L) in.push_back(lg);
     std::sort(in.begin(), in.end(), [&](int a, int b) { return first[a] < first[b]; });
     for (int lg = 0; lg < q.nSV; lg++)
         if (q.l2p[lg] < q.L && !((need0 >> lg) & 1)) out.push_back(lg);
@@ -303,7 +340,7 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
     int gp[8], lp[8], k = 0;
     for (size_t i = 0; i < in.size() && i < out.size() && k < 8; i++) {
         const bool required = (need0 >> in[i]) & 1;
-        if (!required && first[out[i]] <= first[in[i]]) break;
+        if (!required && first[out[i]] < first[in[i]]) break;
         gp[k] = q.l2p[in[i]];
         lp[k] = q.l2p[out[i]];
         k++;

@@ -22,12 +22,12 @@ def _single(name, env):
     return SCENARIOS[name](env)
 
 
-def _multi(name, ranks, tmp_path):
+def _multi(name, ranks, tmp_path, **env):
     from quest_amd.parallel import spawn_local
 
     out = str(tmp_path / f"{name}_{ranks}.npz")
     res = spawn_local([os.path.join(HERE, "dist_worker.py"), name, out], ranks,
-                      env_extra={"QUEST_BACKEND": "cpu", "PYTHONPATH": ROOT}, timeout=600)
+                      env_extra={"QUEST_BACKEND": "cpu", "PYTHONPATH": ROOT, **env}, timeout=600)
     for r, p in enumerate(res):
         assert p.returncode == 0, f"rank {r}:\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
     with np.load(out, allow_pickle=False) as z:
@@ -60,3 +60,14 @@ def test_rank_qubit_relabels(env, tmp_path, ranks):
         np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
     assert int(got["_relabels"]) > 0
     assert int(got["_global_diags"]) > 0
+
+
+@pytest.mark.parametrize("name", ["random_ops_statevector", "measurement_and_collapse", "rank_qubit_gates"])
+def test_sliced_pipelined_exchange(env, tmp_path, name):
+    """Tiny exchange slices (QUEST_EXCHANGE_SLICE_KB=1): every swap runs as
+    many double-buffered slices (pack s+1 / exchange s / unpack s-1) and
+    the canonical-placement restore in several pieces."""
+    want = _single(name, env)
+    got = _multi(name, 4, tmp_path, QUEST_EXCHANGE_SLICE_KB="1")
+    for k, v in want.items():
+        np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
