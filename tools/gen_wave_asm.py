@@ -275,49 +275,46 @@ class Gen:
         T = [self.vp(t) for t in self.T[4 * ts:4 * ts + 4]]
         m = self.sm
         e = self.e
+        # every kind updates the pair in place: products that still need the
+        # old values go to temporaries first, the last op of each output is an
+        # FMA into its own register (no copies back from temporaries)
         if kind == "M2":
-            e(f"v_mul_f64 {T[0]}, {m(0)}, {r0}")
-            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i0}, {T[0]}")
-            e(f"v_fma_f64 {T[0]}, {m(2)}, {r1}, {T[0]}")
-            e(f"v_fma_f64 {T[0]}, -{m(3)}, {i1}, {T[0]}")
-            e(f"v_mul_f64 {T[1]}, {m(0)}, {i0}")
-            e(f"v_fma_f64 {T[1]}, {m(1)}, {r0}, {T[1]}")
-            e(f"v_fma_f64 {T[1]}, {m(2)}, {i1}, {T[1]}")
-            e(f"v_fma_f64 {T[1]}, {m(3)}, {r1}, {T[1]}")
+            # T = m01 b, U = m10 a ; a = m00 a + T ; b = m11 b + U
+            e(f"v_mul_f64 {T[0]}, {m(2)}, {r1}")
+            e(f"v_mul_f64 {T[1]}, {m(2)}, {i1}")
             e(f"v_mul_f64 {T[2]}, {m(4)}, {r0}")
-            e(f"v_fma_f64 {T[2]}, -{m(5)}, {i0}, {T[2]}")
-            e(f"v_fma_f64 {T[2]}, {m(6)}, {r1}, {T[2]}")
-            e(f"v_fma_f64 {T[2]}, -{m(7)}, {i1}, {T[2]}")
             e(f"v_mul_f64 {T[3]}, {m(4)}, {i0}")
+            e(f"v_fma_f64 {T[0]}, -{m(3)}, {i1}, {T[0]}")
+            e(f"v_fma_f64 {T[1]}, {m(3)}, {r1}, {T[1]}")
+            e(f"v_fma_f64 {T[2]}, -{m(5)}, {i0}, {T[2]}")
             e(f"v_fma_f64 {T[3]}, {m(5)}, {r0}, {T[3]}")
+            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i0}, {T[0]}")
+            e(f"v_fma_f64 {T[1]}, {m(1)}, {r0}, {T[1]}")
+            e(f"v_fma_f64 {T[2]}, -{m(7)}, {i1}, {T[2]}")
             e(f"v_fma_f64 {T[3]}, {m(7)}, {r1}, {T[3]}")
+            e(f"v_fma_f64 {r0}, {m(0)}, {r0}, {T[0]}")
+            e(f"v_fma_f64 {i0}, {m(0)}, {i0}, {T[1]}")
+            e(f"v_fma_f64 {r1}, {m(6)}, {r1}, {T[2]}")
             e(f"v_fma_f64 {i1}, {m(6)}, {i1}, {T[3]}")
-            e(f"v_mov_b64 {r1}, {T[2]}")
-            e(f"v_mov_b64 {r0}, {T[0]}")
-            e(f"v_mov_b64 {i0}, {T[1]}")
         elif kind == "M2R":   # m = m00 m01 m10 m11 (real)
-            e(f"v_mul_f64 {T[0]}, {m(0)}, {r0}")
-            e(f"v_fma_f64 {T[0]}, {m(1)}, {r1}, {T[0]}")
+            e(f"v_mul_f64 {T[0]}, {m(1)}, {r1}")
             e(f"v_mul_f64 {T[1]}, {m(2)}, {r0}")
-            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[1]}")
-            e(f"v_mul_f64 {T[2]}, {m(0)}, {i0}")
-            e(f"v_fma_f64 {T[2]}, {m(1)}, {i1}, {T[2]}")
+            e(f"v_mul_f64 {T[2]}, {m(1)}, {i1}")
             e(f"v_mul_f64 {T[3]}, {m(2)}, {i0}")
+            e(f"v_fma_f64 {r0}, {m(0)}, {r0}, {T[0]}")
+            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[1]}")
+            e(f"v_fma_f64 {i0}, {m(0)}, {i0}, {T[2]}")
             e(f"v_fma_f64 {i1}, {m(3)}, {i1}, {T[3]}")
-            e(f"v_mov_b64 {r0}, {T[0]}")
-            e(f"v_mov_b64 {i0}, {T[2]}")
         elif kind == "M2RI":  # m = m00, Im m01, Im m10, m11
-            # a = m0 r0 - m1 i1 ; d = m3 i1 + m2 r0 ; b = m0 i0 + m1 r1 ; c = m3 r1 - m2 i0
-            e(f"v_mul_f64 {T[0]}, {m(0)}, {r0}")
-            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i1}, {T[0]}")
-            e(f"v_mul_f64 {T[1]}, {m(2)}, {r0}")
-            e(f"v_fma_f64 {i1}, {m(3)}, {i1}, {T[1]}")
-            e(f"v_mul_f64 {T[2]}, {m(0)}, {i0}")
-            e(f"v_fma_f64 {T[2]}, {m(1)}, {r1}, {T[2]}")
-            e(f"v_mul_f64 {T[3]}, -{m(2)}, {i0}")
-            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[3]}")
-            e(f"v_mov_b64 {r0}, {T[0]}")
-            e(f"v_mov_b64 {i0}, {T[2]}")
+            # r0 = m0 r0 - m1 i1 ; i0 = m0 i0 + m1 r1 ; r1 = m3 r1 - m2 i0 ; i1 = m3 i1 + m2 r0
+            e(f"v_mul_f64 {T[0]}, -{m(1)}, {i1}")
+            e(f"v_mul_f64 {T[1]}, {m(1)}, {r1}")
+            e(f"v_mul_f64 {T[2]}, -{m(2)}, {i0}")
+            e(f"v_mul_f64 {T[3]}, {m(2)}, {r0}")
+            e(f"v_fma_f64 {r0}, {m(0)}, {r0}, {T[0]}")
+            e(f"v_fma_f64 {i0}, {m(0)}, {i0}, {T[1]}")
+            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[2]}")
+            e(f"v_fma_f64 {i1}, {m(3)}, {i1}, {T[3]}")
         elif kind == "ANTI":  # m = m01 re,im ; m10 re,im
             e(f"v_mul_f64 {T[0]}, {m(0)}, {r1}")
             e(f"v_fma_f64 {T[0]}, -{m(1)}, {i1}, {T[0]}")
