@@ -43,7 +43,7 @@ constexpr int kWaveLanes = 6;   // 64 lanes
 // virtual lane bits 6.. of the tile (transpositions with a slot go through
 // LDS, controls on them are wave-uniform predicates)
 #ifndef QA_WAVE_WBITS
-#define QA_WAVE_WBITS 2
+#define QA_WAVE_WBITS 3
 #endif
 constexpr int kWaveWBits = QA_WAVE_WBITS;
 constexpr int kWaveLaneBits = kWaveLanes + kWaveWBits;  // real + wave lane bits

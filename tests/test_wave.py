@@ -20,7 +20,7 @@ def _run(args, env_extra, timeout=600):
 
 
 def test_wave_plans_emulated_on_host_every_gate_kind():
-    out = _run([os.path.join(ROOT, "tools", "wave_kinds.py"), "--qubits", "13", "--count", "40"],
+    out = _run([os.path.join(ROOT, "tools", "wave_kinds.py"), "--qubits", "15", "--count", "40"],
                {"QUEST_BACKEND": "cpu", "QUEST_CPU_PLANNER": "3"})
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
     assert "bad: []" in out.stdout
@@ -38,7 +38,7 @@ def test_wave_plans_emulated_on_host_random_streams():
 
 @pytest.mark.gpu
 def test_wave_kernel_every_gate_kind_gpu():
-    out = _run([os.path.join(ROOT, "tools", "wave_kinds.py"), "--qubits", "18", "--count", "40"], {}, timeout=300)
+    out = _run([os.path.join(ROOT, "tools", "wave_kinds.py"), "--qubits", "21", "--count", "40"], {}, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
     assert "bad: []" in out.stdout and " wave 0 " not in out.stdout
 

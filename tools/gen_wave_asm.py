@@ -24,6 +24,9 @@ Device records (host side: src/hip/backend_hip.hip, WaveLaunchDev / WaveOpDev):
            + 16   u32 nOps              + 24  u32 pos[16]
            + 88   u64 ldGroupByte[16]   + 216 u64 stGroupByte[16]
            + 344  u32 ldLaneByte[64]    + 600 u32 stLaneByte[64]
+           + 856  u64 ldWaveByte[8]     + 920 u64 stWaveByte[8]
+           + 984  u64 debugBuf
+           pos[b] for b >= 12 sits in bits 8.. of pos[b - 12]
            + 1024 WaveOpDev ops[]  (96 B: i32 handler, u32 cReg, u32 cLane,
                   u32 aux, u64 ctrlOut, u64 pad, f64 m[8])
 Semantics of every op: src/core/wave.hpp (and the CPU emulation in
@@ -35,6 +38,7 @@ import struct
 import sys
 
 KINDS = ["M2", "M2R", "M2RI", "ANTI", "SWAP"]
+LD_WAVE, ST_WAVE, DEBUG_BUF = 856, 920, 984   # launch-record offsets (see above)
 # handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
 def idx_slot(kind, s, ctrl):
     return KINDS.index(kind) * 16 + s * 2 + ctrl          # 0..79
@@ -57,11 +61,11 @@ def idx_diag(creg, lane):
 
 
 def idx_trw(s, b):
-    return 200 + s * 2 + b                                 # 200..(200 + 2R)
+    return 200 + s * 4 + b                                 # 200..(200 + 4R), b < 4
 
 
 def table_size(R):
-    return max(136 + (2 << R), 216)
+    return max(136 + (2 << R), 200 + 4 * R)
 
 
 _VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b|\b(vcc)\b")
@@ -592,12 +596,12 @@ class Gen:
             # i+1 B is copied to A.  Prologue: load the first tile into B.
             self.tile_check("s[16:17]", ".Ldone")
             self.base_of("s[16:17]", 68)
-            self.wave_bytes(856, 70)
+            self.wave_bytes(LD_WAVE, 70)
             if self.debug:
                 # debug: record (wave id, tile, base, load byte offset, lane 0's
-                # lane offset) per wave at launch+920 + 64 * (4 * wg + (s3 & 3))
+                # lane offset) per wave at debugBuf + 64 * (4 * wg + (s3 & 3))
                 # and stop before touching the state
-                e("s_load_dwordx2 s[94:95], s[8:9], 920")     # debug buffer
+                e(f"s_load_dwordx2 s[94:95], s[8:9], {DEBUG_BUF}")     # debug buffer
                 e("s_waitcnt lgkmcnt(0)")
                 e("s_and_b32 s98, s3, 3")
                 e("s_lshl_b32 s99, s2, 2")
@@ -631,7 +635,7 @@ class Gen:
             e("s_addc_u32 s73, s17, s15")
             self.tile_check("s[72:73]", ".Lno_prefetch")
             self.base_of("s[72:73]", 68)
-            self.wave_bytes(856, 70)
+            self.wave_bytes(LD_WAVE, 70)
             self.groups("ld", 88, vldb, NG, self.B, 96)
             self.label(".Lno_prefetch")
         else:
@@ -639,7 +643,7 @@ class Gen:
             self.label(".Ltile_loop")
             self.tile_check("s[16:17]", ".Ldone")
             self.base_of("s[16:17]", 32)
-            self.wave_bytes(856, 34)
+            self.wave_bytes(LD_WAVE, 34)
             self.groups("ld", 88, vldb, NG, 0, 96)
             e("s_waitcnt vmcnt(0)")
         # ---- op loop: prefetch op 0, then every op starts through next_op()
@@ -651,7 +655,7 @@ class Gen:
         self.next_op()
         self.label(".Lops_done")
         e("s_waitcnt lgkmcnt(0)")      # the prefetch past the last op writes s[36:59]
-        self.wave_bytes(888, 34)
+        self.wave_bytes(ST_WAVE, 34)
         self.groups("st", 216, vstb, NG, 0, 96)
         e("s_add_u32 s16, s16, s14")
         e("s_addc_u32 s17, s17, s15")
@@ -709,9 +713,13 @@ class Gen:
         s[d+2:d+3] = the same in bytes."""
         e = self.e
         e(f"s_mov_b64 s[{d}:{d + 1}], {tile}")
-        assert self.R + 6 + self.W <= 12, "pos[] lives in s[20:31]"
-        for b in range(self.R + 6 + self.W):
+        K = self.R + 6 + self.W
+        assert K <= 24, "pos[] lives in s[20:31] (b >= 12 in bits 8..)"
+        for b in range(K):
             p = f"s{20 + b}"
+            if b >= 12:   # the s_*64 shift / bfm operands use bits 5:0 only
+                e(f"s_lshr_b32 s95, s{20 + b - 12}, 8")   # s[94:95] is free outside the op loop
+                p = "s95"
             e(f"s_bfm_b64 s[96:97], {p}, 0")
             e(f"s_and_b64 s[98:99], s[{d}:{d + 1}], s[96:97]")
             e(f"s_lshr_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], {p}")
@@ -847,14 +855,17 @@ def main():
     ap.add_argument("mode", choices=["asm", "embed"])
     ap.add_argument("--slots", type=int, default=4)
     ap.add_argument("--dbuf", type=int, default=-1, help="software-pipelined tiles (default: when 4 slots)")
-    ap.add_argument("--wbits", type=int, default=2, help="2^wbits waves share a tile")
+    ap.add_argument("--wbits", type=int, default=3, help="2^wbits waves share a tile")
     ap.add_argument("--debug", action="store_true", help="record addressing state per wave and stop (no state access)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--obj")
     ap.add_argument("--hsaco")
     args = ap.parse_args()
     if args.mode == "asm":
-        g = Gen(args.slots, args.dbuf if args.dbuf >= 0 else args.slots <= 4, args.wbits, args.debug)
+        # the second register set costs a wave per SIMD: worth it only while
+        # a tile has <= 4 waves (otherwise too few workgroups fit a CU)
+        dbuf = args.dbuf if args.dbuf >= 0 else (args.slots <= 4 and args.wbits <= 2)
+        g = Gen(args.slots, dbuf, args.wbits, args.debug)
         g.kernel()
         with open(args.out, "w") as f:
             f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
@@ -875,6 +886,8 @@ def main():
         f.write("// GENERATED by tools/gen_wave_asm.py embed -- do not edit\n")
         f.write(f"static const int kWaveImageSlots = {args.slots};\n")
         f.write(f"static const int kWaveImageWBits = {args.wbits};\n")
+        vg = re.search(r"amdhsa_next_free_vgpr (\d+)", open(args.out.replace("wave_image.inc", "wave_kernel.s")).read())
+        f.write(f"static const int kWaveImageVgprs = {vg.group(1)};\n")
         f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
         f.write(f"static const unsigned char kWaveImage[{len(img)}] __attribute__((aligned(4096))) = {{\n")
         for k in range(0, len(img), 24):

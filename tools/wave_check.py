@@ -35,7 +35,7 @@ def main():
         from helpers import apply_random_ops, oracle_for
 
         capi.setQuESTTuning("tile_mode", 3)
-        for n in (18, 19, 21):
+        for n in (20, 21, 23):
             rng = np.random.default_rng(n)
             reg = qa.Register(env, n)
             o = oracle_for(reg, rng)
