@@ -230,13 +230,14 @@ def test_reference_golden_suite_on_gpu(genv):
     assert passed >= 770
 
 
-@pytest.mark.parametrize("ranks", [2, 4])
+@pytest.mark.parametrize("ranks,slice_kb", [(2, ""), (4, ""), (4, "1")])
 @pytest.mark.parametrize("name", ["random_ops_statevector", "random_ops_density", "measurement_and_collapse",
-                                  "calculations", "qasm_log"])
-def test_distributed_equivalence_on_gpu(genv, tmp_path, name, ranks):
+                                  "calculations", "qasm_log", "rank_qubit_gates"])
+def test_distributed_equivalence_on_gpu(genv, tmp_path, name, ranks, slice_kb):
     """The distributed router with the HIP kernels (pack/unpack, chunk
     predicates, reductions + allreduce) on ONE GPU shared by 2 / 4 ranks over
-    the QUEST_COMM=socket test transport, against the single-rank HIP run."""
+    the QUEST_COMM=socket test transport, against the single-rank HIP run;
+    slice_kb=1 splits every swap into many double-buffered slices."""
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -249,7 +250,8 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, ranks):
     out = str(tmp_path / f"{name}_{ranks}.npz")
     res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks,
                       env_extra={"QUEST_BACKEND": "hip", "QUEST_COMM": "socket",
-                                 "PYTHONPATH": os.path.dirname(here)}, timeout=600)
+                                 "PYTHONPATH": os.path.dirname(here),
+                                 **({"QUEST_EXCHANGE_SLICE_KB": slice_kb} if slice_kb else {})}, timeout=600)
     for r, p in enumerate(res):
         assert p.returncode == 0, f"rank {r}:\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
     with np.load(out, allow_pickle=False) as z:
