@@ -406,6 +406,18 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
             ld[lane][j] = offsetOf(ps.ldSlot, ps.ldLane, lane, j);
             st[lane][j] = offsetOf(ps.stSlot, ps.stLane, lane, j);
         }
+    static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;  // planner study: op mix per pass
+    if (dump) {
+        int cnt[10] = {0}, trw = 0, ctl = 0;
+        for (int i = ps.opBegin; i < ps.opEnd; i++) {
+            const WaveOp& w = wp.ops[(size_t)i];
+            cnt[w.kind]++;
+            if (w.kind == (int)WKind::TR && w.b >= kWaveLanes) trw++;
+            if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
+        }
+        fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) ctl %d\n",
+                ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw, ctl);
+    }
     TilePass tp;
     tp.k = kWaveBits;
     for (int b = 0; b < kWaveBits; b++) tp.pos[b] = ps.pos[b];

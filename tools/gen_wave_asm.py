@@ -39,6 +39,7 @@ import sys
 
 KINDS = ["M2", "M2R", "M2RI", "ANTI", "SWAP"]
 LD_WAVE, ST_WAVE, DEBUG_BUF = 856, 920, 984   # launch-record offsets (see above)
+OPS_DONE = 255                                 # handler index of the end-of-list sentinel
 # handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
 def idx_slot(kind, s, ctrl):
     return KINDS.index(kind) * 16 + s * 2 + ctrl          # 0..79
@@ -65,7 +66,7 @@ def idx_trw(s, b):
 
 
 def table_size(R):
-    return max(136 + (2 << R), 200 + 4 * R)
+    return OPS_DONE + 1
 
 
 _VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b|\b(vcc)\b")
@@ -230,18 +231,30 @@ class Gen:
     def next_op(self):
         """Start the next op (inlined at the end of every handler: one taken
         branch per op).  Op k+1's record was prefetched into s[36:59] while op
-        k ran; it is moved to s[68:91] and op k+2 is prefetched."""
+        k ran; it is moved to s[68:91] and op k+2 is prefetched.  The list
+        ends with a sentinel record whose handler is the store epilogue; ops
+        that need tile / wave predicates have bit 31 of the handler offset set
+        and take the shared check path (rare)."""
         e = self.e
-        e("s_cmp_ge_u32 s19, s18")
-        e("s_cbranch_scc1 .Lops_done")
         e("s_waitcnt lgkmcnt(0)")
         for k in range(0, 24, 2):
             e(f"s_mov_b64 s[{68 + k}:{69 + k}], s[{36 + k}:{37 + k}]")
-        e("s_add_u32 s19, s19, 1")
         e("s_add_u32 s94, s94, 96")
         e("s_addc_u32 s95, s95, 0")
         e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
         e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
+        e("s_bitcmp1_b32 s68, 31")
+        e("s_cbranch_scc1 .Lcheck")
+        e("s_add_u32 s98, s92, s68")                   # kernel base + handler offset
+        e("s_addc_u32 s99, s93, 0")
+        e("s_setpc_b64 s[98:99]")
+
+    def check_path(self):
+        """Shared slow path of next_op: skip the op (start the next one) unless
+        the tile satisfies its out-of-tile controls and this wave its
+        wave-bit controls, else dispatch it."""
+        e = self.e
+        self.label(".Lcheck")
         e("s_and_b64 s[96:97], s[32:33], s[72:73]")    # ctrlOut of the op
         e("s_cmp_eq_u64 s[96:97], s[72:73]")
         e("s_cbranch_scc0 .Lnext")
@@ -252,7 +265,8 @@ class Gen:
             e("s_and_b32 s96, s3, s75")                 # wave bits that must be 0
             e("s_cmp_eq_u32 s96, 0")
             e("s_cbranch_scc0 .Lnext")
-        e("s_add_u32 s98, s92, s68")                   # kernel base + handler offset
+        e("s_bitset0_b32 s68, 31")
+        e("s_add_u32 s98, s92, s68")
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
 
@@ -481,15 +495,18 @@ class Gen:
             sh = 8 if l == 3 else 4
             lo_banks = "0x3" if l == 3 else "0x5"   # lanes with the bit clear
             hi_banks = "0xc" if l == 3 else "0xa"   # lanes with the bit set
-            for g in range(0, len(pairs), 4):
-                grp = pairs[g:g + 4]
+            # all copies first (32 temporaries), then the DPP moves: one
+            # VALU-write -> DPP-read wait for the whole handler
+            big = [self.T[0] + i for i in range(32)]
+            for g in range(0, len(pairs), 32):
+                grp = pairs[g:g + 32]
                 for k, (a, b) in enumerate(grp):
-                    e(f"v_mov_b32_e32 v{tmp[k]}, v{b}")
+                    e(f"v_mov_b32_e32 v{big[k]}, v{b}")
                 e("s_nop 1")
                 for k, (a, b) in enumerate(grp):
                     # bit clear: b <- partner(lane + sh).a ; bit set: a <- partner(lane - sh).b (old)
                     e(f"v_mov_b32_dpp v{b}, v{a} row_shl:{sh} row_mask:0xf bank_mask:{lo_banks}")
-                    e(f"v_mov_b32_dpp v{a}, v{tmp[k]} row_shr:{sh} row_mask:0xf bank_mask:{hi_banks}")
+                    e(f"v_mov_b32_dpp v{a}, v{big[k]} row_shr:{sh} row_mask:0xf bank_mask:{hi_banks}")
             self.back()
             return
         qp = "[1,0,3,2]" if l == 0 else "[2,3,0,1]"
@@ -578,7 +595,6 @@ class Gen:
         e("s_subb_u32 s93, s93, 0")
         e("s_waitcnt lgkmcnt(0)")
         e("s_load_dwordx4 s[12:15], s[8:9], 0x0")     # numTiles, waveStride
-        e("s_load_dword s18, s[8:9], 0x10")           # nOps
         e("s_load_dwordx8 s[20:27], s[8:9], 0x18")    # pos[0..7]
         e("s_load_dwordx4 s[28:31], s[8:9], 0x38")    # pos[8..11]
         e("s_add_u32 s10, s8, 1024")
@@ -647,13 +663,14 @@ class Gen:
             self.groups("ld", 88, vldb, NG, 0, 96)
             e("s_waitcnt vmcnt(0)")
         # ---- op loop: prefetch op 0, then every op starts through next_op()
-        e("s_mov_b32 s19, 0")
         e("s_mov_b64 s[94:95], s[10:11]")
         e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
         e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
         self.label(".Lnext")
         self.next_op()
-        self.label(".Lops_done")
+        self.check_path()
+        self.label("wh_OPS_DONE")     # the sentinel record's handler
+        self.handlers[OPS_DONE] = "wh_OPS_DONE"
         e("s_waitcnt lgkmcnt(0)")      # the prefetch past the last op writes s[36:59]
         self.wave_bytes(ST_WAVE, 34)
         self.groups("st", 216, vstb, NG, 0, 96)
