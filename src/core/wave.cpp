@@ -1,6 +1,7 @@
 #include "wave.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "router.hpp"
@@ -90,6 +91,19 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         if (needsSlot(i)) nextNeed[(size_t)i * kWaveBits + ops[i].t[0]] = i;
     }
     auto nextUse = [&](int i, int b) { return nextNeed[(size_t)i * kWaveBits + b]; };
+    // remaining[i][b]: ops >= i needing tile bit b in a slot
+    std::vector<int> remaining((size_t)(nOps + 1) * kWaveBits, 0);
+    for (int i = nOps - 1; i >= 0; i--) {
+        for (int b = 0; b < kWaveBits; b++)
+            remaining[(size_t)i * kWaveBits + b] = remaining[(size_t)(i + 1) * kWaveBits + b];
+        if (needsSlot(i)) remaining[(size_t)i * kWaveBits + ops[i].t[0]]++;
+    }
+    // a gate on lane bit 0-2 runs there directly (DPP partner fetch: about one
+    // transposition of work, twice a slot gate) unless the bit has enough slot
+    // uses left in the pass to pay for a transposition in -- and, for tile
+    // bits 1-3, the one back before the store; QUEST_WAVE_LANE_OPS=0 disables
+    static const bool laneOps = !getenv("QUEST_WAVE_LANE_OPS") || atoi(getenv("QUEST_WAVE_LANE_OPS")) != 0;
+    auto laneOpsMax = [&](int b) { return !laneOps ? 0 : (b >= 1 && b <= 3) ? 4 : 2; };
 
     WavePass wp;
     for (int i = 0; i < kWaveBits; i++) wp.pos[i] = ps.pos[i];
@@ -116,6 +130,11 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // if the rest has fewer, near bits leave the slots for them and far bits
     // of the rest take their slot places
     std::vector<int> lanes, waves;
+    // lanes 3-5 take the lowest positions of the rest: a 16-byte load / store
+    // of 64 lanes then spans the fewest DRAM pages and translations
+    // (QUEST_WAVE_LANE_ORDER=0: in need order instead)
+    static const bool byPos = !getenv("QUEST_WAVE_LANE_ORDER") || atoi(getenv("QUEST_WAVE_LANE_ORDER")) != 0;
+    if (byPos) std::sort(rest.begin(), rest.end());
     for (int b : rest)
         if (!farPos(b) && (int)lanes.size() < kWaveLanes - 3) lanes.push_back(b);
         else waves.push_back(b);
@@ -191,6 +210,39 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 w.m[2] = m[6];
                 w.m[3] = m[7];
             }
+            w.ctrlOut = op.ctrlOut;
+            out.ops.push_back(w);
+            continue;
+        }
+        if (!inSlot(lay.where[t]) && laneOf(lay.where[t]) < kWaveLaneOps && cls[i] != M2Class::General &&
+            remaining[(size_t)i * kWaveBits + t] <= laneOpsMax(t)) {
+            WaveOp w;
+            switch (cls[i]) {
+                case M2Class::Swap: w = blank((int)WKind::LSWAP); break;
+                case M2Class::Anti:
+                    w = blank((int)WKind::LANTI);
+                    w.m[0] = m[2];
+                    w.m[1] = m[3];
+                    w.m[2] = m[4];
+                    w.m[3] = m[5];
+                    break;
+                case M2Class::Real:
+                    w = blank((int)WKind::LM2R);
+                    w.m[0] = m[0];
+                    w.m[1] = m[2];
+                    w.m[2] = m[4];
+                    w.m[3] = m[6];
+                    break;
+                default:
+                    w = blank((int)WKind::LM2RI);
+                    w.m[0] = m[0];
+                    w.m[1] = m[3];
+                    w.m[2] = m[5];
+                    w.m[3] = m[6];
+                    break;
+            }
+            w.a = laneOf(lay.where[t]);
+            masks(lay, op.ctrlIn, w.cReg, w.cLane);
             w.ctrlOut = op.ctrlOut;
             out.ops.push_back(w);
             continue;

@@ -60,7 +60,14 @@ enum class WKind : int {
     D2S = 6,   // diagonal 2x2 on the bit of slot a (m = d0 re,im, d1 re,im)
     D2L = 7,   // diagonal 2x2 on lane bit a
     TR = 8,    // transpose slot a with lane bit b (b >= 6: wave bit, through LDS; never masked)
+    // the same gates with their target on real lane bit a < kWaveLaneOps (lane
+    // pairs combined through DPP, per-lane coefficients; m as for the slot kinds)
+    LM2R = 9,
+    LM2RI = 10,
+    LANTI = 11,
+    LSWAP = 12,
 };
+constexpr int kWaveLaneOps = 3;  // lane bits with direct gate handlers
 
 // One op, uploaded as-is (uniform: read through the scalar cache).
 struct WaveOp {

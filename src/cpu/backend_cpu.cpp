@@ -331,6 +331,47 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         return;
     }
     const real* m = w.m;
+    if (kind >= WKind::LM2R) {
+        // target on lane bit a: lane pairs (L0, L1 = L0 | 2^a), per register
+        const int a = w.a;
+        for (int L0 = 0; L0 < kVLanes; L0++) {
+            if ((L0 >> a) & 1) continue;
+            if (((unsigned)L0 & w.cLane) != w.cLane || ((unsigned)L0 & w.cLaneZero)) continue;
+            const int L1 = L0 | (1 << a);
+            for (int j = 0; j < kWaveRegs; j++) {
+                if (((unsigned)j & w.cReg) != w.cReg) continue;
+                const real r0 = vr[L0][j], i0 = vi[L0][j], r1 = vr[L1][j], i1 = vi[L1][j];
+                real *R0 = &vr[L0][j], *I0 = &vi[L0][j], *R1 = &vr[L1][j], *I1 = &vi[L1][j];
+                switch (kind) {
+                    case WKind::LM2R:
+                        *R0 = m[0] * r0 + m[1] * r1;
+                        *I0 = m[0] * i0 + m[1] * i1;
+                        *R1 = m[2] * r0 + m[3] * r1;
+                        *I1 = m[2] * i0 + m[3] * i1;
+                        break;
+                    case WKind::LM2RI:
+                        *R0 = m[0] * r0 - m[1] * i1;
+                        *I0 = m[0] * i0 + m[1] * r1;
+                        *R1 = m[3] * r1 - m[2] * i0;
+                        *I1 = m[3] * i1 + m[2] * r0;
+                        break;
+                    case WKind::LANTI:
+                        *R0 = m[0] * r1 - m[1] * i1;
+                        *I0 = m[0] * i1 + m[1] * r1;
+                        *R1 = m[2] * r0 - m[3] * i0;
+                        *I1 = m[2] * i0 + m[3] * r0;
+                        break;
+                    default:  // LSWAP
+                        *R0 = r1;
+                        *I0 = i1;
+                        *R1 = r0;
+                        *I1 = i0;
+                        break;
+                }
+            }
+        }
+        return;
+    }
     for (int lane = 0; lane < kVLanes; lane++) {
         if (((unsigned)lane & w.cLane) != w.cLane) continue;
         if ((unsigned)lane & w.cLaneZero) continue;
@@ -391,6 +432,8 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
     }
 }
 
+long long g_trCost = 0;  // QUEST_WAVE_DUMP: weighted transposition cost (planner study)
+
 void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {
     static thread_local i64 ld[kVLanes][kWaveRegs], st[kVLanes][kWaveRegs];
     auto offsetOf = [&](const int* slotBit, const int* laneBit, int lane, int j) {
@@ -408,15 +451,18 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
         }
     static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;  // planner study: op mix per pass
     if (dump) {
-        int cnt[10] = {0}, trw = 0, ctl = 0;
+        int cnt[16] = {0}, trw = 0, ctl = 0;
         for (int i = ps.opBegin; i < ps.opEnd; i++) {
             const WaveOp& w = wp.ops[(size_t)i];
             cnt[w.kind]++;
             if (w.kind == (int)WKind::TR && w.b >= kWaveLanes) trw++;
+            if (w.kind == (int)WKind::TR) g_trCost += waveTransposeCost(w.b);
             if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
         }
-        fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) ctl %d\n",
-                ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw, ctl);
+        fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d ctl %d\n",
+                ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
+                cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl);
+        fprintf(stderr, "wave: cumulative weighted transposition cost %lld\n", g_trCost);
     }
     TilePass tp;
     tp.k = kWaveBits;

@@ -39,7 +39,7 @@ import sys
 
 KINDS = ["M2", "M2R", "M2RI", "ANTI", "SWAP"]
 LD_WAVE, ST_WAVE, DEBUG_BUF = 856, 920, 984   # launch-record offsets (see above)
-OPS_DONE = 255                                 # handler index of the end-of-list sentinel
+OPS_DONE = 256                                 # handler index of the end-of-list sentinel
 # handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
 def idx_slot(kind, s, ctrl):
     return KINDS.index(kind) * 16 + s * 2 + ctrl          # 0..79
@@ -59,6 +59,14 @@ def idx_tr(s, l):
 
 def idx_diag(creg, lane):
     return 136 + creg * 2 + lane                           # 136..(136 + 2^(R+1))
+
+
+# gates applied on lane bits directly (general 2x2 and lane bits >= 3 transpose)
+LANE_KINDS, LANE_BITS = ["M2R", "M2RI", "ANTI", "SWAP"], 3
+
+
+def idx_lane(kind, l, ctrl):
+    return 216 + KINDS.index(kind) * 8 + l * 2 + ctrl     # 216..255: gates on lane bits 0-3
 
 
 def idx_trw(s, b):
@@ -180,7 +188,8 @@ class Gen:
         self.T = [D + 2 * k for k in range(16)]
         self.C0, self.C1 = D + 32, D + 34
         self.vLane, self.vLdB, self.vStB, self.vTmp = D + 36, D + 37, D + 38, D + 39
-        self.nvgpr = D + 40      # 168 for R = 4: three waves per SIMD
+        self.CL = D + 40         # 4 doubles: per-lane coefficients of the lane-bit gates
+        self.nvgpr = D + 48      # 112 for R = 4 without the second register set: 4 waves per SIMD
         self.handlers = {}
         self.buf = None          # straight-line region being collected for scheduling
 
@@ -524,6 +533,130 @@ class Gen:
             # the next group's DPPs read other registers: no hazard
         self.back()
 
+    # ---- gates on lane bits 0-3 (no transposition) --------------------
+    def lane_fetch(self, l, dst, src):
+        """dst dword <- the partner lane's (lane ^ 2^l) src dword."""
+        if l < 2:
+            qp = "[1,0,3,2]" if l == 0 else "[2,3,0,1]"
+            self.e(f"v_mov_b32_dpp v{dst}, v{src} quad_perm:{qp} row_mask:0xf bank_mask:0xf")
+            return
+        sh = 8 if l == 3 else 4
+        lo, hi = ("0x3", "0xc") if l == 3 else ("0x5", "0xa")
+        self.e(f"v_mov_b32_dpp v{dst}, v{src} row_shl:{sh} row_mask:0xf bank_mask:{lo}")
+        self.e(f"v_mov_b32_dpp v{dst}, v{src} row_shr:{sh} row_mask:0xf bank_mask:{hi}")
+
+    def lane_coeffs(self, kind, l):
+        """Per-lane coefficients (vcc = lanes with bit l set): CS multiplies
+        the lane's own amplitude, CP the partner's."""
+        e = self.e
+        e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, {l}, 1")
+        e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
+        CL, C0 = self.CL, self.C0
+
+        def sel(dst, k_clear, k_set):
+            e(f"v_mov_b64 {self.vp(dst)}, {self.sm(k_clear)}")
+            e(f"v_mov_b64 {self.vp(C0)}, {self.sm(k_set)}")
+            e(f"v_cndmask_b32_e32 v{dst}, v{dst}, v{C0}, vcc")
+            e(f"v_cndmask_b32_e32 v{dst + 1}, v{dst + 1}, v{C0 + 1}, vcc")
+        if kind in ("M2R", "M2RI"):      # m00 m01 m10 m11 (M2RI: the off-diagonals imaginary)
+            sel(CL, 0, 3)
+            sel(CL + 2, 1, 2)
+        elif kind == "ANTI":             # m01 re,im ; m10 re,im
+            sel(CL + 4, 0, 2)
+            sel(CL + 6, 1, 3)
+        elif kind == "M2":               # m00, m01, m10, m11 complex
+            sel(CL, 0, 6)
+            sel(CL + 2, 1, 7)
+            sel(CL + 4, 2, 4)
+            sel(CL + 6, 3, 5)
+
+    def lane_math(self, kind, j, px, py, B=None):
+        x, y = self.vp(self.re(j)), self.vp(self.im(j))
+        CS, CP = self.vp(self.CL), self.vp(self.CL + 2)
+        CSr, CSi, CPr, CPi = (self.vp(self.CL + 2 * k) for k in range(4))
+        e = self.e
+        px, py = self.vp(px), self.vp(py)
+        if kind == "M2R":
+            e(f"v_mul_f64 {px}, {CP}, {px}")
+            e(f"v_mul_f64 {py}, {CP}, {py}")
+            e(f"v_fma_f64 {x}, {CS}, {x}, {px}")
+            e(f"v_fma_f64 {y}, {CS}, {y}, {py}")
+        elif kind == "M2RI":
+            e(f"v_mul_f64 {py}, -{CP}, {py}")
+            e(f"v_mul_f64 {px}, {CP}, {px}")
+            e(f"v_fma_f64 {x}, {CS}, {x}, {py}")
+            e(f"v_fma_f64 {y}, {CS}, {y}, {px}")
+        elif kind == "ANTI":
+            CPr, CPi = self.vp(self.CL + 4), self.vp(self.CL + 6)
+            e(f"v_mul_f64 {x}, {CPr}, {px}")
+            e(f"v_mul_f64 {y}, {CPr}, {py}")
+            e(f"v_fma_f64 {x}, -{CPi}, {py}, {x}")
+            e(f"v_fma_f64 {y}, {CPi}, {px}, {y}")
+        elif kind == "M2":
+            B = self.vp(B)
+            e(f"v_mul_f64 {B}, {CPr}, {py}")
+            e(f"v_fma_f64 {B}, {CPi}, {px}, {B}")
+            e(f"v_mul_f64 {px}, {CPr}, {px}")
+            e(f"v_fma_f64 {px}, -{CPi}, {py}, {px}")
+            e(f"v_fma_f64 {px}, -{CSi}, {y}, {px}")
+            e(f"v_fma_f64 {B}, {CSi}, {x}, {B}")
+            e(f"v_fma_f64 {x}, {CSr}, {x}, {px}")
+            e(f"v_fma_f64 {y}, {CSr}, {y}, {B}")
+
+    def gen_lane(self, kind, l, ctrl):
+        """A one-qubit gate whose target is lane bit l: every lane combines
+        its own amplitude with its partner's (lane ^ 2^l, fetched by DPP)
+        using per-lane coefficients, in place -- instead of transposing the
+        bit into a slot and back (2 x 64-128 VALU)."""
+        self.handler(idx_lane(kind, l, ctrl), f"L{kind}_l{l}_c{ctrl}")
+        e = self.e
+        e("s_nop 1")   # VALU write -> DPP read of the same VGPR
+        NS = self.NS
+        if kind != "SWAP":
+            self.lane_coeffs(kind, l)
+        if ctrl:
+            self.ctrl_begin()
+        per = 3 if kind == "M2" else 2        # temporaries (doubles) per amplitude
+        batch = 1 if ctrl else (4 if kind == "M2" else 8)
+        for j0 in range(0, NS, batch):
+            js = list(range(j0, j0 + batch))
+            skip = f".Lskip_L{kind}_{l}_{j0}"
+            if ctrl:
+                self.ctrl_j(j0, skip)
+            if kind == "SWAP":
+                for j in js:
+                    regs = [self.re(j), self.re(j) + 1, self.im(j), self.im(j) + 1]
+                    if l < 2:
+                        for r in regs:   # in place: DPP reads every lane before writing
+                            self.lane_fetch(l, r, r)
+                    else:
+                        tmp = [self.T[0] + k for k in range(4)]
+                        for r, t in zip(regs, tmp):
+                            e(f"v_mov_b32_e32 v{t}, v{r}")
+                        e("s_nop 1")
+                        for r, t in zip(regs, tmp):
+                            self.lane_fetch(l, r, t)
+            else:
+                slots = []
+                for k, j in enumerate(js):
+                    px, py = self.T[per * k], self.T[per * k + 1]
+                    B = self.T[per * k + 2] if kind == "M2" else None
+                    for d in (0, 1):
+                        self.lane_fetch(l, px + d, self.re(j) + d)
+                        self.lane_fetch(l, py + d, self.im(j) + d)
+                    slots.append((j, px, py, B))
+                if not ctrl:
+                    self.region()
+                for j, px, py, B in slots:
+                    self.lane_math(kind, j, px, py, B)
+                if not ctrl:
+                    self.end_region()
+            if ctrl:
+                self.label(skip)
+        if ctrl:
+            self.ctrl_end()
+        self.back()
+
     def gen_trw(self, s, b):
         """Transpose slot s with wave bit b through LDS: the wave with the bit
         clear sends its registers with slot bit s set and receives the
@@ -700,6 +833,10 @@ class Gen:
         for s in range(1, R):
             for b in range(self.W):
                 self.gen_trw(s, b)
+        for kind in LANE_KINDS:
+            for l in range(LANE_BITS):
+                for c in (0, 1):
+                    self.gen_lane(kind, l, c)
         L.append(".Lfunc_end0:")
         L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
         self.descriptor()
