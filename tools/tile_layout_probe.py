@@ -37,6 +37,9 @@ def main():
         "0-3 + 10-18": [0, 1, 2, 3] + list(range(10, 19)),
         "0-3 + 4-6 + top 6": [0, 1, 2, 3, 4, 5, 6] + list(range(n - 6, n)),
         "0-6 + 18-23": list(range(7)) + list(range(18, 24)),
+        "0-3 + 9-17": [0, 1, 2, 3] + list(range(9, 18)),
+        "0-3 + 14-22": [0, 1, 2, 3] + list(range(14, 23)),
+        "0-3 + 4-6 + 12-17": [0, 1, 2, 3, 4, 5, 6] + list(range(12, 18)),
     }
     traffic = 2 * 16 * (1 << n)
     for name, qs in sets.items():
