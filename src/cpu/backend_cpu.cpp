@@ -564,7 +564,8 @@ void flush(QuregImpl& q) {
     }();
     const bool wave = planner == 3 && q.L >= kWaveBits;
     fuseBlockQubits() = wave ? 1 : 2;
-    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), 4, rt().fusion, prog);
+    static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : 5;  // as the HIP backend
+    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? waveCmin : 4, rt().fusion, prog);
     if (trace::on())
         trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
                      q.pending.size(), prog.passes.size());
