@@ -24,10 +24,10 @@ Device records (host side: src/hip/backend_hip.hip, WaveLaunchDev / WaveOpDev):
            + 16   u32 nOps              + 24  u32 pos[16]
            + 88   u64 ldGroupByte[16]   + 216 u64 stGroupByte[16]
            + 344  u32 ldLaneByte[64]    + 600 u32 stLaneByte[64]
-           + 856  u64 ldWaveByte[8]     + 920 u64 stWaveByte[8]
-           + 984  u64 debugBuf
+           + 1024 u64 ldWaveByte[16]    + 1152 u64 stWaveByte[16]
+           + 1280 u64 debugBuf
            pos[b] for b >= 12 sits in bits 8.. of pos[b - 12]
-           + 1024 WaveOpDev ops[]  (96 B: i32 handler, u32 cReg, u32 cLane,
+           + 2048 WaveOpDev ops[]  (96 B: i32 handler, u32 cReg, u32 cLane,
                   u32 aux, u64 ctrlOut, u64 pad, f64 m[8])
 Semantics of every op: src/core/wave.hpp (and the CPU emulation in
 src/cpu/backend_cpu.cpp applyWaveOp, which the tests compare against).
@@ -38,7 +38,7 @@ import struct
 import sys
 
 KINDS = ["M2", "M2R", "M2RI", "ANTI", "SWAP"]
-LD_WAVE, ST_WAVE, DEBUG_BUF = 856, 920, 984   # launch-record offsets (see above)
+LD_WAVE, ST_WAVE, DEBUG_BUF, OPS_OFF = 1024, 1152, 1280, 2048   # launch-record offsets (see above)
 OPS_DONE = 256                                 # handler index of the end-of-list sentinel
 # handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
 def idx_slot(kind, s, ctrl):
@@ -730,7 +730,7 @@ class Gen:
         e("s_load_dwordx4 s[12:15], s[8:9], 0x0")     # numTiles, waveStride
         e("s_load_dwordx8 s[20:27], s[8:9], 0x18")    # pos[0..7]
         e("s_load_dwordx4 s[28:31], s[8:9], 0x38")    # pos[8..11]
-        e("s_add_u32 s10, s8, 1024")
+        e(f"s_add_u32 s10, s8, {OPS_OFF}")
         e("s_addc_u32 s11, s9, 0")
         e(f"v_lshlrev_b32_e32 v{vt}, 2, v{vl}")
         e(f"global_load_dword v{vldb}, v{vt}, s[8:9] offset:344")
