@@ -201,12 +201,14 @@ def main():
     todo = args.only.split(",")
     if "tutorial" in todo:
         run_tutorial(env, res)
-    if "sweep" in todo:
-        run_sweep(env, res, args.max_qubits)
-    if "random30" in todo:
-        run_random30(env, res)
+    # the 30-qubit programs first: after the sweep frees 256 GiB, the next
+    # allocation pays the driver's page clearing on first touch
     if "fork30" in todo:
         run_fork30(env, res)
+    if "random30" in todo:
+        run_random30(env, res)
+    if "sweep" in todo:
+        run_sweep(env, res, args.max_qubits)
     if "q34" in todo and args.max_qubits >= 34:
         run_q34(env, res)
     if "density17" in todo and args.max_qubits >= 34:
