@@ -57,8 +57,10 @@ def test_all_gates_vs_oracle(genv, n):
     reg.close()
 
 
-@pytest.mark.parametrize("n", [3, 5, 7])
+@pytest.mark.parametrize("n", [3, 5, 7, 10])
 def test_density_gates_and_noise(genv, n):
+    """n = 10 (2^20 amplitudes): the wave engine runs the gates and the LDS
+    kernel the channels, flushed as alternating runs of the mixed queue."""
     import quest_amd as qa
     from helpers import apply_random_ops, assert_close, oracle_for
 
