@@ -39,6 +39,11 @@ import sys
 
 KINDS = ["M2", "M2R", "M2RI", "ANTI", "SWAP"]
 LD_WAVE, ST_WAVE, DEBUG_BUF, OPS_OFF = 1024, 1152, 1280, 2048   # launch-record offsets (see above)
+import os as _os
+# cache policy of the state stream (non-temporal by default); WAVE_LD_POLICY /
+# WAVE_ST_POLICY override for experiments, e.g. "" or " sc1"
+LD_POLICY = _os.environ.get("WAVE_LD_POLICY", " nt")
+ST_POLICY = _os.environ.get("WAVE_ST_POLICY", " nt")
 OPS_DONE = 256                                 # handler index of the end-of-list sentinel
 # handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
 def idx_slot(kind, s, ctrl):
@@ -908,9 +913,9 @@ class Gen:
                 e(f"s_add_u32 s{Q}, s{Q}, s{g}")
                 e(f"s_addc_u32 s{Q + 1}, s{Q + 1}, s{g + 1}")
                 if what == "ld":
-                    e(f"buffer_load_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen nt")
+                    e(f"buffer_load_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen{LD_POLICY}")
                 else:
-                    e(f"buffer_store_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen nt")
+                    e(f"buffer_store_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen{ST_POLICY}")
 
     def descriptor(self):
         nv = self.nvgpr
