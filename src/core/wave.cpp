@@ -133,8 +133,23 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // lanes 3-5 take the lowest positions of the rest: a 16-byte load / store
     // of 64 lanes then spans the fewest DRAM pages and translations
     // (QUEST_WAVE_LANE_ORDER=0: in need order instead)
-    static const bool byPos = !getenv("QUEST_WAVE_LANE_ORDER") || atoi(getenv("QUEST_WAVE_LANE_ORDER")) != 0;
-    if (byPos) std::sort(rest.begin(), rest.end());
+    // (QUEST_WAVE_LANE_ORDER=2: the wave bits -- LDS transpositions -- take the
+    // latest-needed of the rest first, lanes 3-5 the others by position)
+    static const int laneOrder = getenv("QUEST_WAVE_LANE_ORDER") ? atoi(getenv("QUEST_WAVE_LANE_ORDER")) : 1;
+    if (laneOrder == 2) {
+        std::vector<int> byNeed(rest);  // need order already; latest last
+        std::vector<int> wv;
+        for (int x = (int)byNeed.size() - 1; x >= 0 && (int)wv.size() < kWaveWBits; x--) wv.push_back(byNeed[x]);
+        std::vector<int> ln;
+        for (int b : rest)
+            if (std::find(wv.begin(), wv.end(), b) == wv.end()) ln.push_back(b);
+        std::sort(ln.begin(), ln.end());
+        rest = ln;
+        rest.insert(rest.end(), wv.begin(), wv.end());
+        // far bits among the lane candidates still go to waves below
+    } else if (laneOrder == 1) {
+        std::sort(rest.begin(), rest.end());
+    }
     for (int b : rest)
         if (!farPos(b) && (int)lanes.size() < kWaveLanes - 3) lanes.push_back(b);
         else waves.push_back(b);

@@ -28,6 +28,18 @@ def test_wave_plans_emulated_on_host_every_gate_kind():
     assert " wave 0 " not in out.stdout, out.stdout
 
 
+@pytest.mark.parametrize("knobs", [{"QUEST_WAVE_LANE_OPS": "0"}, {"QUEST_WAVE_LANE_ORDER": "0"},
+                                   {"QUEST_WAVE_LANE_ORDER": "2"}, {"QUEST_WAVE_CMIN": "7"}])
+def test_wave_plan_variants_emulated_on_host(knobs):
+    """Planner variants (lane-bit gates off, lane / wave bit assignment
+    orders, more always-in-tile bits) give the same states."""
+    out = _run([os.path.join(ROOT, "tools", "wave_kinds.py"), "--qubits", "15", "--count", "24",
+                "--kinds", "h,x,y,rx,ry,rz,t,cnot,cy,cz,ccompact,mcunitary"],
+               dict({"QUEST_BACKEND": "cpu", "QUEST_CPU_PLANNER": "3"}, **knobs))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
+    assert "bad: []" in out.stdout
+
+
 def test_wave_plans_emulated_on_host_random_streams():
     """Random mixed streams (all gate kinds, controls on any bit) and the
     fusion / golden suites through the wave planner."""
