@@ -432,6 +432,32 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         // candidates: plain in-order greedy, and greedy seeded with the high
         // targets of one of the next few ops; keep the pass holding most ops
         u64 bestHigh = scan(0, best);
+        // candidate score: ops taken, plus a bonus for ops from the front of
+        // the queue (deferring them blocks everything behind them)
+        static const double alpha = getenv("QUEST_PLAN_ALPHA") ? atof(getenv("QUEST_PLAN_ALPHA")) : 0.0;
+        static const int frontN = getenv("QUEST_PLAN_FRONT") ? atoi(getenv("QUEST_PLAN_FRONT")) : 32;
+        int frontEnd = first;
+        for (int c = 0; frontEnd < n && c < frontN; frontEnd++)
+            if (!done[frontEnd]) c++;
+        static const double beta = getenv("QUEST_PLAN_LOOKAHEAD") ? atof(getenv("QUEST_PLAN_LOOKAHEAD")) : 0.0;
+        std::vector<int> nextTake;
+        auto score = [&](const std::vector<int>& v) {
+            int f = 0;
+            for (int i : v) f += i < frontEnd;
+            double sc = (double)v.size() + alpha * f;
+            if (beta > 0) {
+                // one-pass lookahead: how much the plain greedy pass after it takes
+                for (int i : v) done[i] = 1;
+                const int keepFirst = first;
+                while (first < n && done[first]) first++;
+                if (first < n) scan(0, nextTake); else nextTake.clear();
+                first = keepFirst;
+                for (int i : v) done[i] = 0;
+                sc += beta * (double)nextTake.size();
+            }
+            return sc;
+        };
+        double bestScore = score(best);
         static const int maxSeeds = [] {
             const char* e = getenv("QUEST_PLAN_SEEDS");
             return e ? atoi(e) : 24;
@@ -449,9 +475,11 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             if (dup || nTried == 16) continue;
             tried[nTried++] = h;
             const u64 hh = scan(h, take);
-            if (take.size() > best.size()) {
+            const double sc = score(take);
+            if (sc > bestScore) {
                 best.swap(take);
                 bestHigh = hh;
+                bestScore = sc;
             }
         }
         for (int i : best) {
