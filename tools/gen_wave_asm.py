@@ -741,7 +741,31 @@ class Gen:
         e(f"global_load_dword v{vldb}, v{vt}, s[8:9] offset:344")
         e(f"global_load_dword v{vstb}, v{vt}, s[8:9] offset:600")
         # first tile = workgroup (one wave each)
+        # first tile of this workgroup.  The dispatcher deals workgroups to the
+        # 8 XCDs round-robin, then to the CUs of an XCD, then a second round
+        # (P per CU): with the host's map word (launch + 20: bit 31 enable,
+        # bits 0-7 log2 CUs per XCD, 8-15 log2 P) workgroup w takes tile
+        # (w % 8) * C * P + ((w / 8) % C) * P + w / (8 C): the P workgroups of
+        # a CU take adjacent tiles and an XCD a contiguous block -- they share
+        # pages (address translations) instead of each touching its own
+        e("s_load_dword s99, s[8:9], 0x14")
+        e("s_waitcnt lgkmcnt(0)")
         e("s_mov_b32 s16, s2")
+        e("s_bitcmp1_b32 s99, 31")
+        e("s_cbranch_scc0 .Lmap_done")
+        e("s_bfe_u32 s97, s99, 0x80000")             # log2 C (bits 0-7)
+        e("s_bfe_u32 s96, s99, 0x80008")             # log2 P (bits 8-15)
+        e("s_lshr_b32 s98, s2, 3")                   # r = w / 8
+        e("s_bfm_b32 s95, s97, 0")                   # C - 1
+        e("s_and_b32 s95, s98, s95")                 # cu = r % C
+        e("s_lshr_b32 s98, s98, s97")                # slot = r / C
+        e("s_lshl_b32 s95, s95, s96")                # cu * P
+        e("s_add_u32 s98, s98, s95")                 # cu * P + slot
+        e("s_add_u32 s95, s97, s96")                 # log2 (C P)
+        e("s_and_b32 s16, s2, 7")
+        e("s_lshl_b32 s16, s16, s95")                # (w % 8) C P
+        e("s_add_u32 s16, s16, s98")
+        self.label(".Lmap_done")
         e("s_mov_b32 s17, 0")
         e("s_waitcnt vmcnt(0) lgkmcnt(0)")
         if self.dbuf:
