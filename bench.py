@@ -12,7 +12,18 @@ tutorial_example.c:29-518).  `value` = wall seconds per gate over the timed
 steps (max over ranks), gates applied through the public API exactly as a
 user would call them (hadamard(), rotateX(), controlledNot(), ...).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--qubits Q] [--eager]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--qubits Q] [--eager] [--no-extras]
+
+Besides the headline, a single-GPU run adds (outside the timed region, ~10 s):
+  * ``sweep``: the metric's "vs #qubits" axis -- unfused Hadamard on targets
+    0, n/2, n-1 and T on n/2 for n = 20, 22, ..., 32 (median of 5, one
+    streaming pass per gate), with the achieved HBM bandwidth;
+  * ``fork30``: the fork's own 30-qubit program end to end (490 gates, 30
+    calcProbOfOutcome, 10 getAmp; tutorial_example.c:1-3, 29-534);
+  * ``window1_s_per_gate``: the headline circuit flushed after every layer
+    (the scheduler sees one layer at a time, as in a program that reads the
+    state between layers).
+A multi-GPU run must use RCCL (``--allow-transport`` accepts another one).
 """
 from __future__ import annotations
 
@@ -37,6 +48,8 @@ def main():
     ap.add_argument("--qubits", type=int, default=30, help="qubits per GPU")
     ap.add_argument("--eager", action="store_true", help="disable gate fusion (one pass per gate)")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--no-extras", action="store_true", help="skip sweep / fork30 / one-layer window")
+    ap.add_argument("--allow-transport", action="store_true", help="accept a non-RCCL transport with N > 1")
     args = ap.parse_args()
 
     from quest_amd.parallel import allreduce_max, barrier, init_distributed
@@ -56,6 +69,10 @@ def main():
     if args.eager:
         os.environ["QUEST_FUSION"] = "0"
     env = qa.Env()
+    transport = qa.capi.getQuESTTransport()
+    if world > 1 and not transport.startswith("RCCL") and not args.allow_transport:
+        print(f"bench.py: {world} ranks must exchange over RCCL, transport is '{transport}'", file=sys.stderr)
+        sys.exit(3)
     n = args.qubits + int(round(math.log2(world)))
     reg = qa.Register(env, n)
     reg.init_plus()
@@ -111,6 +128,9 @@ def main():
     qa.capi.setGateFusion(1)
     unfused_gate_s = allreduce_max(sorted(singles)[2])
     s_per_gate = elapsed / max(gates, 1)
+    extras = {}
+    if world == 1 and not args.no_extras and qa.capi.getQuESTBackend() == "HIP":
+        extras = run_extras(qa, reg, n, layer_gates, args)
     result = {
         "metric": "single-qubit-gate time (s) vs #qubits, fp64 state-vector; 1/2/4/8-GPU scaling",
         "value": s_per_gate,
@@ -132,18 +152,85 @@ def main():
             "seq_len": 1 << n,
             "gates_per_step": gates / max(args.steps, 1),
             "parallelism": f"dp{world}: amplitude-sharded over {world} GPU(s), qubit swaps over RCCL",
-            "transport": qa.capi.getQuESTTransport(),
+            "transport": transport,
             "fusion": not args.eager,
             "passes": stats["passes"],
             "swaps": stats["swaps"],
             "norm_error": abs(norm - 1.0),
             "unfused_gate_s": unfused_gate_s,
             "backend": qa.capi.getQuESTBackend(),
+            **extras,
         },
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
     reg.close()
+
+
+def _median_time(fn, reps=5):
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2]
+
+
+def run_extras(qa, reg, n, layer_gates, args):
+    """Sweep, fork30 and one-layer window (single GPU, outside the timed
+    region; see the module docstring)."""
+    from quest_amd.models import fork_circuit
+    from quest_amd.models.circuits import Circuit
+
+    out = {}
+    # one-layer window: the same layers, flushed one at a time
+    t0 = time.perf_counter()
+    g = 0
+    for s in range(args.steps):
+        Circuit(n, layer_gates[args.warmup + s]).apply(reg)
+        reg.flush()
+        g += len(layer_gates[args.warmup + s])
+    reg.sync()
+    out["window1_s_per_gate"] = (time.perf_counter() - t0) / max(g, 1)
+    # fork program on a fresh register (the bench register stays allocated)
+    fork = fork_circuit()
+    f = qa.Register(reg.envobj, 30)
+    f.init_zero()
+    f.sync()
+    t0 = time.perf_counter()
+    fork.apply(f)
+    f.sync()
+    t1 = time.perf_counter()
+    probs = [f.prob(q, 1) for q in range(30)]
+    t2 = time.perf_counter()
+    amps = [f.amp(i) for i in range(10)]
+    t3 = time.perf_counter()
+    out["fork30"] = {"total_s": t3 - t0, "gates_s": t1 - t0, "probs_s": t2 - t1, "amps_s": t3 - t2,
+                     "gates": len(fork.gates), "p_q0": probs[0], "amp0": [amps[0].real, amps[0].imag]}
+    f.close()
+    # unfused single-qubit gate time vs #qubits
+    qa.capi.setGateFusion(0)
+    sweep = []
+    for m in range(20, 33, 2):
+        r = qa.Register(reg.envobj, m)
+        r.init_plus()
+        r.sync()
+        row = {"n": m}
+        for name, t in (("h0", 0), ("hmid", m // 2), ("htop", m - 1), ("tmid", m // 2)):
+            gate = r.h if name[0] == "h" else r.t
+
+            def one():
+                gate(t)
+                r.sync()
+
+            one()  # warm
+            row[name + "_ms"] = 1e3 * _median_time(one)
+        row["hmid_TBps"] = 2 * 16 * (1 << m) / (row["hmid_ms"] * 1e-3) / 1e12
+        sweep.append(row)
+        r.close()
+    qa.capi.setGateFusion(1)
+    out["sweep"] = sweep
+    return out
 
 
 if __name__ == "__main__":

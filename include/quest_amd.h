@@ -38,6 +38,8 @@ void setFusionMaxQubits(int numQubits);
  * key is known.  Also settable at start via QUEST_DIRECT_KERNELS /
  * QUEST_TILE_MODE / QUEST_TILE_QUBITS / QUEST_TILE_WG_PER_CU / ... */
 int setQuESTTuning(const char* key, int value);
+/* Current value of a tuning knob (into *value); returns 1 if the key is known. */
+int getQuESTTuning(const char* key, int* value);
 
 /* Submit every queued operation of the register to the device (async). */
 void flushQureg(Qureg qureg);
@@ -67,6 +69,21 @@ void getAmps(Qureg qureg, long long int startInd, qreal* reals, qreal* imags, lo
 int saveQuregCheckpoint(Qureg qureg, const char* path);
 int loadQuregCheckpoint(Qureg qureg, const char* path);
 
+/* Per-rank device memory a register of numQubitsInStateVec qubits needs on
+ * numRanks ranks (0: the current number), in bytes: out = {state (re + im of the
+ * chunk), exchange slice buffers of distributed swaps, scratch, total}.
+ * createQureg / createDensityQureg check the total against the free device
+ * memory (E_OUT_OF_MEMORY with this breakdown); QUEST_DEVICE_MEM_MB overrides
+ * the free amount. */
+void getQuregMemoryPlan(int numQubitsInStateVec, int numRanks, long long out[4]);
+
+/* Diagnostic: drive the device transport's code paths (HIP build: RCCL with a
+ * one-rank communicator -- pipelined exchange on the communication stream,
+ * scalar allreduce / broadcast, allgather, async-error polling) and check the
+ * data.  Single-process jobs only.  Returns 1 if everything matched; a
+ * description goes to report. */
+int runCommSelfTest(char* report, int reportLen);
+
 /* Restore the canonical qubit layout after distributed qubit remapping. */
 void canonicaliseQureg(Qureg qureg);
 /* physical bit position of each logical qubit of the state-vector */
@@ -85,6 +102,7 @@ typedef struct QuESTStats {
     long long waveTransposes; /* cross-lane transpositions among them */
     long long relabels;       /* X/Y-like gates on rank qubits applied by relabelling chunks (no data moved) */
     long long globalDiags;    /* diagonal one-qubit gates on rank qubits applied as per-rank scalings */
+    long long flushes;        /* backend queue flushes (each planned into fused passes) */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

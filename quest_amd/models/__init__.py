@@ -9,4 +9,5 @@ from .circuits import (  # noqa: F401
     ghz,
     qft,
     random_layered,
+    random_mixed,
 )

@@ -91,6 +91,23 @@ class Circuit:
             else:
                 raise ValueError(g.name)
 
+    def inverse(self) -> "Circuit":
+        """The adjoint circuit: gates reversed, each replaced by its inverse
+        (so ``c`` followed by ``c.inverse()`` is the identity)."""
+        inv = Circuit(self.n)
+        for g in reversed(self.gates):
+            if g.name in ("h", "x", "y", "z", "cnot", "cy", "cz", "mcz"):
+                inv.gates.append(Gate(g.name, g.qubits))
+            elif g.name == "s":
+                inv.gates.append(Gate("phase", g.qubits, -math.pi / 2))
+            elif g.name == "t":
+                inv.gates.append(Gate("phase", g.qubits, -math.pi / 4))
+            elif g.param is not None:
+                inv.gates.append(Gate(g.name, g.qubits, -g.param))
+            else:
+                raise ValueError(f"no inverse for {g.name}")
+        return inv
+
     def to_qasm(self) -> str:
         lines = ["OPENQASM 2.0;", f"qreg q[{self.n}];", f"creg c[{self.n}];"]
         for g in self.gates:
@@ -117,6 +134,45 @@ def random_layered(n: int, depth: int, seed: int = 0, entangle: bool = True) -> 
         if entangle:
             for a in range(layer % 2, n - 1, 2):
                 c.add("cnot", a, a + 1)
+    return c
+
+
+def random_mixed(n: int, num_gates: int, seed: int = 0, high: int = 0) -> Circuit:
+    """`num_gates` random gates mixing one-qubit gates, controlled gates,
+    controlled rotations and multi-controlled phase flips.  With high > 0,
+    targets and controls are drawn from the top `high` qubits two times in
+    three (tile bits far above the low, always-resident positions)."""
+    rng = np.random.default_rng(seed)
+    c = Circuit(n)
+    top = list(range(max(0, n - high), n)) if high > 0 else []
+
+    def qubit():
+        if top and rng.random() < 2 / 3:
+            return int(top[rng.integers(len(top))])
+        return int(rng.integers(n))
+
+    def distinct(k):
+        out = []
+        while len(out) < k:
+            q = qubit()
+            if q not in out:
+                out.append(q)
+        return out
+
+    kinds = ONE_QUBIT + ("phase", "cnot", "cy", "cz", "crx", "cry", "crz", "cphase", "mcz")
+    for _ in range(num_gates):
+        name = kinds[rng.integers(len(kinds))]
+        angle = float(rng.uniform(0, 2 * math.pi))
+        if name in ("rx", "ry", "rz", "phase"):
+            c.add(name, qubit(), param=angle)
+        elif name in ONE_QUBIT:
+            c.add(name, qubit())
+        elif name in ("cnot", "cy", "cz"):
+            c.add(name, *distinct(2))
+        elif name == "mcz":
+            c.add(name, *distinct(int(rng.integers(2, 5))))
+        else:
+            c.add(name, *distinct(2), param=angle)
     return c
 
 

@@ -81,7 +81,7 @@ class _Binding:
             _fields_ = [(n, C.c_longlong) for n in
                         ("opsQueued", "passes", "fusedOps", "swaps", "bytesExchanged", "reductions",
                          "verifiedFlushes", "wavePasses", "waveOps", "waveTransposes", "relabels",
-                         "globalDiags")]
+                         "globalDiags", "flushes")]
 
         self.Complex, self.ComplexMatrix2, self.Vector = Complex, ComplexMatrix2, Vector
         self.ComplexArray, self.QASMLogger, self.Qureg = ComplexArray, QASMLogger, Qureg
@@ -140,7 +140,8 @@ class _Binding:
             "setDensityAmps": (v, [Q, rp, rp]), "getQuEST_PREC": (i, []),
             # MI355X extensions
             "setGateFusion": (v, [i]), "getGateFusion": (i, []), "setFusionMaxQubits": (v, [i]),
-            "setQuESTTuning": (i, [C.c_char_p, i]),
+            "setQuESTTuning": (i, [C.c_char_p, i]), "getQuESTTuning": (i, [C.c_char_p, ip]),
+            "getQuregMemoryPlan": (v, [i, i, P(ll)]), "runCommSelfTest": (i, [C.c_char_p, i]),
             "flushQureg": (v, [Q]), "syncQureg": (v, [Q]), "copyStateToGPU": (v, [Q]),
             "copyStateFromGPU": (v, [Q]), "copyChunkToBuffers": (v, [Q, C.c_void_p, C.c_void_p]),
             "copyChunkFromBuffers": (v, [Q, C.c_void_p, C.c_void_p]), "canonicaliseQureg": (v, [Q]),
@@ -416,6 +417,27 @@ def getQuESTStats() -> dict:
 
 def setQuESTTuning(key: str, value: int) -> bool:
     return bool(_call("setQuESTTuning", key.encode(), int(value)))
+
+
+def getQuregMemoryPlan(num_qubits_in_statevec: int, num_ranks: int = 0) -> dict:
+    """Per-rank device bytes of a register on num_ranks ranks (0: this job's):
+    state, exchange, scratch, total."""
+    out = (C.c_longlong * 4)()
+    _call("getQuregMemoryPlan", int(num_qubits_in_statevec), int(num_ranks), out)
+    return dict(zip(("state", "exchange", "scratch", "total"), list(out)))
+
+
+def runCommSelfTest():
+    """(ok, report) of the device transport self-test (quest_amd.h)."""
+    buf = C.create_string_buffer(512)
+    ok = _call("runCommSelfTest", buf, 512)
+    return bool(ok), buf.value.decode()
+
+
+def getQuESTTuning(key: str):
+    """Current value of a tuning knob, or None if the build does not know it."""
+    v = C.c_int(0)
+    return v.value if _call("getQuESTTuning", key.encode(), C.byref(v)) else None
 
 
 def getQuESTBackend() -> str:

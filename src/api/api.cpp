@@ -76,6 +76,27 @@ void fillQuregStruct(Qureg& q, QuregImpl& m) {
     q.qasmLog = &m.log;
 }
 
+// The per-rank memory a register needs (router::memoryPlan) against what
+// the device has free: fail with the breakdown rather than die in hipMalloc
+// or, for distributed registers, at the first swap's buffer allocation.
+bool memoryBudget(int nSV, const char* caller) {
+    const router::MemoryPlan m = router::memoryPlan(nSV, rt().numRanks);
+    size_t freeB = 0, totalB = 0;
+    bool known = be::memoryInfo(&freeB, &totalB);
+    if (const char* e = getenv("QUEST_DEVICE_MEM_MB")) {
+        freeB = (size_t)atoll(e) << 20;
+        known = true;
+    }
+    if (!known || (long long)freeB >= m.total) return true;
+    char detail[256];
+    const double G = 1024.0 * 1024 * 1024;
+    snprintf(detail, sizeof detail,
+             "%d qubits on %d rank(s) need %.2f GiB per rank: state %.2f + exchange buffers %.2f + scratch %.2f; "
+             "%.2f GiB free",
+             nSV, rt().numRanks, m.total / G, m.state / G, m.exchange / G, m.scratch / G, freeB / G);
+    return raiseErrorMsg(E_OUT_OF_MEMORY, caller, detail);
+}
+
 Qureg makeQureg(int nSV, bool density, int nRep) {
     QuregImpl* m = new QuregImpl();
     m->magic = kQuregMagic;
@@ -268,6 +289,7 @@ Qureg createQureg(int numQubits, QuESTEnv env) {
     Qureg q;
     memset(&q, 0, sizeof q);
     if (!v::createNumQubits(numQubits, rt().numRanks, __func__)) return q;
+    if (!memoryBudget(numQubits, __func__)) return q;
     q = makeQureg(numQubits, false, numQubits);
     initZeroState(q);
     return q;
@@ -279,6 +301,7 @@ Qureg createDensityQureg(int numQubits, QuESTEnv env) {
     memset(&q, 0, sizeof q);
     if (!v::createNumQubits(numQubits, 1, __func__)) return q;
     if (!v::createNumQubits(2 * numQubits, rt().numRanks, __func__)) return q;
+    if (!memoryBudget(2 * numQubits, __func__)) return q;
     q = makeQureg(2 * numQubits, true, numQubits);
     initZeroState(q);
     return q;
@@ -916,6 +939,19 @@ int setQuESTTuning(const char* key, int value) {
     return be::setTuning(key, value) ? 1 : 0;
 }
 
+int getQuESTTuning(const char* key, int* value) {
+    int v = 0;
+    bool known = true;
+    if (key && !strcmp(key, "fuse_blocks"))
+        v = fuseBlocks() ? 1 : 0;
+    else if (key && !strcmp(key, "verify"))
+        v = rt().verify ? 1 : 0;
+    else
+        known = be::getTuning(key, &v);
+    if (known && value) *value = v;
+    return known ? 1 : 0;
+}
+
 void flushQureg(Qureg qureg) { router::flush(Q(qureg)); }
 void syncQureg(Qureg qureg) { router::sync(Q(qureg)); }
 
@@ -954,6 +990,21 @@ void getAmps(Qureg qureg, long long int startInd, qreal* reals, qreal* imags, lo
     router::readRange(Q(qureg), startInd, reals, imags, numAmps);
 }
 
+int runCommSelfTest(char* report, int reportLen) {
+    std::string r;
+    const bool ok = comm::selfTest(r);
+    if (report && reportLen > 0) snprintf(report, (size_t)reportLen, "%s", r.c_str());
+    return ok ? 1 : 0;
+}
+
+void getQuregMemoryPlan(int numQubitsInStateVec, int numRanks, long long out[4]) {
+    const router::MemoryPlan m = router::memoryPlan(numQubitsInStateVec, numRanks > 0 ? numRanks : rt().numRanks);
+    out[0] = m.state;
+    out[1] = m.exchange;
+    out[2] = m.scratch;
+    out[3] = m.total;
+}
+
 void canonicaliseQureg(Qureg qureg) { router::canonicalise(Q(qureg)); }
 
 void getQubitLayout(Qureg qureg, int* physicalOfLogical) {
@@ -974,6 +1025,7 @@ void getQuESTStats(QuESTStats* s) {
     s->waveTransposes = stats().waveTransposes;
     s->relabels = stats().relabels;
     s->globalDiags = stats().globalDiags;
+    s->flushes = stats().flushes;
 }
 
 void resetQuESTStats(void) { stats() = Stats(); }

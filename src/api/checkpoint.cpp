@@ -84,6 +84,10 @@ extern "C" int saveQuregCheckpoint(Qureg qureg, const char* path) {
     return ok;
 }
 
+// Every source file this rank will read is opened and validated (header
+// fields agree with the rank-0 header and the register, file long enough for
+// its chunk) BEFORE the register is touched, so a missing, truncated or
+// foreign file leaves the state as it was.
 extern "C" int loadQuregCheckpoint(Qureg qureg, const char* path) {
     QuregImpl& q = *impl(qureg);
     // the writer's rank count comes from the rank-0 file
@@ -96,30 +100,54 @@ extern "C" int loadQuregCheckpoint(Qureg qureg, const char* path) {
         v::fileOpened(0, __func__);
         return 0;
     }
-    if (h0.numQubits != q.nRep || h0.isDensity != (q.isDensity ? 1 : 0) || h0.realBytes != (int)sizeof(real) ||
-        h0.ampsTotal != q.numAmpsTotal) {
+    int match = h0.numQubits == q.nRep && h0.isDensity == (q.isDensity ? 1 : 0) &&
+                h0.realBytes == (int)sizeof(real) && h0.ampsTotal == q.numAmpsTotal && h0.numChunks > 0 &&
+                h0.ampsPerChunk > 0 && (i64)h0.numChunks * h0.ampsPerChunk == h0.ampsTotal;
+    if (comm::active()) match = comm::allreduceAnd(match);
+    if (!match) {
         raiseError(E_CHECKPOINT_MISMATCH, __func__);
         return 0;
     }
-    router::prepareOverwrite(q);
     const i64 srcChunk = h0.ampsPerChunk;
     const i64 c0 = (i64)q.chunkId * q.numAmpsPerChunk, c1 = c0 + q.numAmpsPerChunk;
-    std::vector<real> re((size_t)std::min(kSlice, q.numAmpsPerChunk)), im(re.size());
-    for (int s = (int)(c0 / srcChunk); ok && s < h0.numChunks && (i64)s * srcChunk < c1; s++) {
+    struct Src {
+        int chunk;
+        FILE* f;
+    };
+    std::vector<Src> srcs;
+    for (int s = (int)(c0 / srcChunk); s < h0.numChunks && (i64)s * srcChunk < c1; s++) {
         FILE* f = fopen(fileOf(path, s).c_str(), "rb");
         CkptHeader h;
-        ok = f != nullptr && readHeader(f, h) && h.chunkId == s && h.ampsPerChunk == srcChunk;
-        const i64 s0 = (i64)s * srcChunk;
+        bool good = f != nullptr && readHeader(f, h) && h.chunkId == s && h.ampsPerChunk == srcChunk &&
+                    h.numChunks == h0.numChunks && h.numQubits == h0.numQubits && h.isDensity == h0.isDensity &&
+                    h.realBytes == h0.realBytes && h.ampsTotal == h0.ampsTotal;
+        if (good) {
+            const long long need = (long long)sizeof h + 2ll * (long long)sizeof(real) * srcChunk;
+            good = fseeko(f, 0, SEEK_END) == 0 && (long long)ftello(f) >= need;
+        }
+        if (f) srcs.push_back({s, f});
+        ok = ok && good;
+    }
+    if (comm::active()) ok = comm::allreduceAnd(ok);
+    if (!ok) {
+        for (Src& x : srcs) fclose(x.f);
+        v::fileOpened(0, __func__);
+        return 0;
+    }
+    router::prepareOverwrite(q);
+    std::vector<real> re((size_t)std::min(kSlice, q.numAmpsPerChunk)), im(re.size());
+    for (Src& x : srcs) {
+        const i64 s0 = (i64)x.chunk * srcChunk;
         const i64 lo = std::max(c0, s0), hi = std::min(c1, s0 + srcChunk);
         for (i64 g = lo; ok && g < hi; g += kSlice) {
             const i64 n = std::min(kSlice, hi - g);
-            const long reOff = (long)(sizeof h + sizeof(real) * (size_t)(g - s0));
-            const long imOff = (long)(sizeof h + sizeof(real) * (size_t)(srcChunk + g - s0));
-            ok = fseek(f, reOff, SEEK_SET) == 0 && fread(re.data(), sizeof(real), (size_t)n, f) == (size_t)n &&
-                 fseek(f, imOff, SEEK_SET) == 0 && fread(im.data(), sizeof(real), (size_t)n, f) == (size_t)n;
+            const off_t reOff = (off_t)(sizeof(CkptHeader) + sizeof(real) * (size_t)(g - s0));
+            const off_t imOff = (off_t)(sizeof(CkptHeader) + sizeof(real) * (size_t)(srcChunk + g - s0));
+            ok = fseeko(x.f, reOff, SEEK_SET) == 0 && fread(re.data(), sizeof(real), (size_t)n, x.f) == (size_t)n &&
+                 fseeko(x.f, imOff, SEEK_SET) == 0 && fread(im.data(), sizeof(real), (size_t)n, x.f) == (size_t)n;
             if (ok) be::writeAmps(q, g - c0, re.data(), im.data(), n);
         }
-        if (f) fclose(f);
+        fclose(x.f);
     }
     if (comm::active()) ok = comm::allreduceAnd(ok);
     if (!ok) v::fileOpened(0, __func__);

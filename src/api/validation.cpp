@@ -1,6 +1,7 @@
 // Validation layer: reference semantics (QuEST/src/QuEST_validation.c:82-263),
 // including its quirks (damping reuses the depolarising error code; the
 // unitarity tolerance is REAL_EPS).
+#include <string>
 #include "validation.hpp"
 
 #include <cmath>
@@ -56,7 +57,9 @@ const char* errorMessage(ErrorCode code) {
 
 bool raiseErrorMsg(ErrorCode code, const char* caller, const char* detail) {
     if (g_handler) {
-        g_handler((int)code, errorMessage(code), caller);
+        std::string msg = errorMessage(code);
+        if (detail) msg += std::string(" (") + detail + ")";
+        g_handler((int)code, msg.c_str(), caller);
         return false;
     }
     printf("!!!\n");

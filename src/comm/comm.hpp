@@ -27,6 +27,9 @@ void discover(int* rank, int* size, int* localRank);
 void init(int rank, int size);
 void finalize();
 bool active();  // true when size > 1
+// A buffer from be::allocComm is about to be freed (transports that cache
+// per-buffer state, e.g. IPC handles, drop it).
+void bufferFreed(const void* p);
 
 // Exchange `bytes` with `peer`: send from `send`, receive into `recv`
 // (both backend comm buffers; must not overlap).
@@ -59,6 +62,9 @@ void bcastHost(void* buf, size_t bytes, int root);
 void allgather(const void* send, void* recv, size_t bytesPerRank);
 void barrier();
 std::string describe();
+// Run the device transport's own code paths with a one-rank communicator
+// (HIP build: RCCL); false with a reason if unavailable or wrong.
+bool selfTest(std::string& report);
 
 }  // namespace comm
 

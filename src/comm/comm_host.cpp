@@ -18,6 +18,7 @@ void finalize() {
     g_size = 1;
 }
 bool active() { return g_size > 1; }
+void bufferFreed(const void*) {}
 void sendrecv(int peer, const void* send, void* recv, size_t bytes) { sock::sendrecv(peer, send, recv, bytes); }
 void exchange(const Xfer* x, int n) {
     for (int i = 0; i < n; i++) sock::sendrecv(x[i].peer, x[i].send, x[i].recv, x[i].bytes);
@@ -35,6 +36,10 @@ void allgather(const void* send, void* recv, size_t bytesPerRank) { sock::allgat
 void barrier() {
     double d = 1;
     sock::allreduceSum(&d, 1);
+}
+bool selfTest(std::string& report) {
+    report = "host build: no device transport";
+    return false;
 }
 std::string describe() { return g_size > 1 ? "TCP socket mesh (host build)" : "single process"; }
 

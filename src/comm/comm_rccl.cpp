@@ -13,9 +13,13 @@
 // PyTorch we bind to torch's RCCL (same HIP runtime); standalone C programs
 // get /opt/rocm's.
 //
-// QUEST_COMM=socket selects the test transport instead: the TCP socket mesh
-// of comm_socket.cpp with every device buffer staged through pinned host
-// memory, so that several ranks can share one GPU (RCCL refuses that).
+// Other transports, only on explicit request (a communicator that fails to
+// come up is a fatal error, never a silent downgrade):
+//   QUEST_COMM=ipc     ranks sharing one GPU: device buffers exchanged through
+//                      HIP IPC handles with the SAME communication stream and
+//                      event protocol (comm_ipc.hpp), scalars over sockets;
+//   QUEST_COMM=socket  the TCP socket mesh of comm_socket.cpp with every
+//                      device buffer staged through pinned host memory.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -28,6 +32,7 @@
 
 #include "../hip/qa_hip.h"
 #include "comm.hpp"
+#include "comm_ipc.hpp"
 
 namespace qa {
 namespace comm {
@@ -54,6 +59,8 @@ struct Rccl {
 } R;
 
 int g_rank = 0, g_size = 1;
+enum class Mode { Single, Rccl, Ipc, Socket };
+Mode g_mode = Mode::Single;
 bool g_socket = false;          // QUEST_COMM=socket test transport
 char* g_stage = nullptr;        // pinned staging for the socket transport
 size_t g_stageBytes = 0;
@@ -141,6 +148,15 @@ double commTimeout() {
 }
 
 void watchdog(double elapsed) {
+    if (g_mode == Mode::Ipc) {
+        if (commTimeout() > 0 && elapsed > commTimeout()) {
+            fprintf(stderr, "QuEST: rank %d: no progress for %.0f s (QUEST_COMM_TIMEOUT) -- a peer rank may have "
+                            "failed\n", g_rank, elapsed);
+            fflush(stderr);
+            exit(EXIT_FAILURE);
+        }
+        return;
+    }
     if (!g_comm) return;
     if (R.getAsyncError) {
         ncclResult_t r = ncclSuccess;
@@ -170,19 +186,43 @@ char* stage(size_t bytes) {
 
 }  // namespace
 
+void createStreams() {
+    QA_HIP_CHECK(hipMalloc(&g_dScalars, sizeof(double) * 64));
+    QA_HIP_CHECK(hipHostMalloc(&g_hScalars, sizeof(double) * 64, hipHostMallocDefault));
+    QA_HIP_CHECK(hipStreamCreateWithFlags(&g_cstream, hipStreamNonBlocking));
+    QA_HIP_CHECK(hipEventCreateWithFlags(&g_ready, hipEventDisableTiming));
+    for (hipEvent_t& e : g_done) QA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipk::setSyncWatchdog(watchdog);
+}
+
 void init(int rank, int size) {
     g_rank = rank;
     g_size = size;
+    g_mode = Mode::Single;
     if (size == 1) return;
     const char* mode = getenv("QUEST_COMM");
-    g_socket = mode && !strcmp(mode, "socket");
-    if (g_socket) {
+    const std::string m = mode ? mode : "rccl";
+    if (m == "socket") {
+        g_mode = Mode::Socket;
+        g_socket = true;
         sock::init(rank, size);
         return;
     }
+    if (m == "ipc") {
+        g_mode = Mode::Ipc;
+        sock::init(rank, size);
+        ipc::init(rank, size);
+        createStreams();
+        return;
+    }
+    if (m != "rccl") {
+        fprintf(stderr, "QuEST: unknown QUEST_COMM=%s (rccl, ipc or socket)\n", mode);
+        exit(EXIT_FAILURE);
+    }
     // RCCL unique id from rank 0; then every rank reports whether its
-    // communicator came up, and if any did not, all fall back together to
-    // the socket transport (staged through host memory) rather than hang
+    // communicator came up.  If any did not, every rank stops with the
+    // reason: a job launched for RCCL over xGMI must not quietly continue on
+    // a host-staged transport (QUEST_COMM=ipc / socket select those).
     int ok = loadRccl() ? 1 : 0;
     ncclUniqueId id;
     memset(&id, 0, sizeof id);
@@ -193,97 +233,119 @@ void init(int rank, int size) {
     std::vector<int> oks(size, 0);
     boot::allgather(rank, size, &ok, oks.data(), sizeof(int));
     for (int r = 0; r < size; r++) ok = ok && oks[r];  // rank 0 failing to make an id fails everyone
+    std::string why = ok ? "" : "librccl could not be loaded or ncclGetUniqueId failed";
     if (ok) {
         const ncclResult_t rc = R.commInitRank(&g_comm, size, id, rank);
         int mine = rc == ncclSuccess ? 1 : 0;
         if (!mine) fprintf(stderr, "QuEST: ncclCommInitRank failed on rank %d: %s\n", rank, R.errorString(rc));
         boot::allgather(rank, size, &mine, oks.data(), sizeof(int));
         for (int r = 0; r < size; r++) ok = ok && oks[r];
-        if (!ok && mine) {
-            R.commDestroy(g_comm);
+        if (!ok) {
+            why = "ncclCommInitRank failed on a rank (several ranks on one GPU? use QUEST_COMM=ipc)";
+            if (mine) R.commDestroy(g_comm);
             g_comm = nullptr;
         }
     }
     if (!ok) {
-        if (rank == 0) fprintf(stderr, "QuEST: RCCL unavailable, using the socket transport (slow)\n");
-        g_socket = true;
-        sock::init(rank, size);
-        return;
+        fprintf(stderr, "QuEST: rank %d: the RCCL transport could not start: %s; set QUEST_COMM=ipc or "
+                        "QUEST_COMM=socket to use another transport explicitly\n", rank, why.c_str());
+        fflush(stderr);
+        exit(EXIT_FAILURE);
     }
-    QA_HIP_CHECK(hipMalloc(&g_dScalars, sizeof(double) * 64));
-    QA_HIP_CHECK(hipHostMalloc(&g_hScalars, sizeof(double) * 64, hipHostMallocDefault));
-    QA_HIP_CHECK(hipStreamCreateWithFlags(&g_cstream, hipStreamNonBlocking));
-    QA_HIP_CHECK(hipEventCreateWithFlags(&g_ready, hipEventDisableTiming));
-    for (hipEvent_t& e : g_done) QA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    hipk::setSyncWatchdog(watchdog);
+    g_mode = Mode::Rccl;
+    createStreams();
 }
 
 void finalize() {
-    if (g_socket) {
-        sock::finalize();
-        if (g_stage) (void)hipHostFree(g_stage);
-        g_stage = nullptr;
-        g_stageBytes = 0;
-        g_socket = false;
+    if (g_mode == Mode::Single) {
+        g_size = 1;
+        return;
     }
-    if (g_comm) {
+    if (g_cstream) {
         hipk::syncStream();
+        (void)hipStreamSynchronize(g_cstream);
         hipk::setSyncWatchdog(nullptr);
-        R.commDestroy(g_comm);
-        g_comm = nullptr;
-        if (g_cstream) {
-            (void)hipStreamSynchronize(g_cstream);
-            (void)hipEventDestroy(g_ready);
-            for (hipEvent_t e : g_done) (void)hipEventDestroy(e);
-            (void)hipStreamDestroy(g_cstream);
-            g_cstream = nullptr;
-        }
+    }
+    if (g_mode == Mode::Ipc) ipc::finalize();
+    if (g_mode == Mode::Socket || g_mode == Mode::Ipc) sock::finalize();
+    if (g_stage) (void)hipHostFree(g_stage);
+    g_stage = nullptr;
+    g_stageBytes = 0;
+    g_socket = false;
+    if (g_comm) R.commDestroy(g_comm);
+    g_comm = nullptr;
+    if (g_cstream) {
+        (void)hipEventDestroy(g_ready);
+        for (hipEvent_t e : g_done) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(g_cstream);
+        g_cstream = nullptr;
         (void)hipFree(g_dScalars);
         (void)hipHostFree(g_hScalars);
         g_dScalars = g_hScalars = nullptr;
     }
+    g_mode = Mode::Single;
     g_size = 1;
 }
 
 bool active() { return g_size > 1; }
+
+void bufferFreed(const void* p) {
+    if (g_mode == Mode::Ipc) ipc::forget(p);
+}
+
+namespace {
+
+// The device-side exchange of one slice set on `stream` (RCCL: one group,
+// every peer's xGMI link at once; IPC: pulls from the peers' buffers).
+// `producer` is the stream whose queued work filled the send buffers.
+void deviceExchange(const Xfer* x, int n, int slot, hipStream_t producer, hipStream_t stream) {
+    if (g_mode == Mode::Ipc) {
+        ipc::transfer(x, n, slot, producer, stream);
+        return;
+    }
+    QA_NCCL(R.groupStart(), "ncclGroupStart");
+    for (int i = 0; i < n; i++) {
+        QA_NCCL(R.send(x[i].send, x[i].bytes, ncclUint8, x[i].peer, g_comm, stream), "ncclSend");
+        QA_NCCL(R.recv(x[i].recv, x[i].bytes, ncclUint8, x[i].peer, g_comm, stream), "ncclRecv");
+    }
+    QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+}
+
+// host staging of a device exchange for the socket transport
+void socketExchange(const Xfer& x) {
+    char* h = stage(2 * x.bytes);
+    QA_HIP_CHECK(hipMemcpyAsync(h, x.send, x.bytes, hipMemcpyDeviceToHost, S()));
+    hipk::syncStream();
+    sock::sendrecv(x.peer, h, h + x.bytes, x.bytes);
+    QA_HIP_CHECK(hipMemcpyAsync(x.recv, h + x.bytes, x.bytes, hipMemcpyHostToDevice, S()));
+    hipk::syncStream();
+}
+
+}  // namespace
 
 void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
     if (peer == g_rank) {
         QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, S()));
         return;
     }
-    if (g_socket) {
-        char* h = stage(2 * bytes);
-        QA_HIP_CHECK(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, S()));
-        hipk::syncStream();
-        sock::sendrecv(peer, h, h + bytes, bytes);
-        QA_HIP_CHECK(hipMemcpyAsync(recv, h + bytes, bytes, hipMemcpyHostToDevice, S()));
-        hipk::syncStream();
-        return;
-    }
-    QA_NCCL(R.groupStart(), "ncclGroupStart");
-    QA_NCCL(R.send(send, bytes, ncclUint8, peer, g_comm, S()), "ncclSend");
-    QA_NCCL(R.recv(recv, bytes, ncclUint8, peer, g_comm, S()), "ncclRecv");
-    QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+    const Xfer x{peer, send, recv, bytes};
+    if (g_mode == Mode::Socket)
+        socketExchange(x);
+    else
+        deviceExchange(&x, 1, 0, S(), S());
 }
 
 void exchange(const Xfer* x, int n) {
-    if (g_socket || g_size == 1) {
+    if (g_mode == Mode::Socket || g_mode == Mode::Single) {
         for (int i = 0; i < n; i++) sendrecv(x[i].peer, x[i].send, x[i].recv, x[i].bytes);
         return;
     }
-    // one group: RCCL drives every peer's xGMI link at once
-    QA_NCCL(R.groupStart(), "ncclGroupStart");
-    for (int i = 0; i < n; i++) {
-        QA_NCCL(R.send(x[i].send, x[i].bytes, ncclUint8, x[i].peer, g_comm, S()), "ncclSend");
-        QA_NCCL(R.recv(x[i].recv, x[i].bytes, ncclUint8, x[i].peer, g_comm, S()), "ncclRecv");
-    }
-    QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+    deviceExchange(x, n, 0, S(), S());
 }
 
 bool pipelined() {
     static const bool off = getenv("QUEST_EXCHANGE_PIPELINE") && atoi(getenv("QUEST_EXCHANGE_PIPELINE")) == 0;
-    return !off && !g_socket && g_size > 1 && g_cstream;
+    return !off && (g_mode == Mode::Rccl || g_mode == Mode::Ipc) && g_cstream;
 }
 
 void exchangeAsync(const Xfer* x, int n, int slot) {
@@ -291,14 +353,12 @@ void exchangeAsync(const Xfer* x, int n, int slot) {
         exchange(x, n);
         return;
     }
+    // the communication stream starts after everything queued so far on the
+    // compute stream (the packs of this slice, the unpacks that freed its
+    // receive buffers)
     QA_HIP_CHECK(hipEventRecord(g_ready, S()));
     QA_HIP_CHECK(hipStreamWaitEvent(g_cstream, g_ready, 0));
-    QA_NCCL(R.groupStart(), "ncclGroupStart");
-    for (int i = 0; i < n; i++) {
-        QA_NCCL(R.send(x[i].send, x[i].bytes, ncclUint8, x[i].peer, g_comm, g_cstream), "ncclSend");
-        QA_NCCL(R.recv(x[i].recv, x[i].bytes, ncclUint8, x[i].peer, g_comm, g_cstream), "ncclRecv");
-    }
-    QA_NCCL(R.groupEnd(), "ncclGroupEnd");
+    deviceExchange(x, n, slot, S(), g_cstream);
     QA_HIP_CHECK(hipEventRecord(g_done[slot & 1], g_cstream));
 }
 
@@ -307,12 +367,9 @@ void exchangeWait(int slot) {
     QA_HIP_CHECK(hipStreamWaitEvent(S(), g_done[slot & 1], 0));
 }
 
-void allreduceSum(double* vals, int n) {
-    if (g_size == 1) return;
-    if (g_socket) {
-        sock::allreduceSum(vals, n);
-        return;
-    }
+namespace {
+// RCCL collectives on host values staged through the device scratch
+void rcclAllreduceSum(double* vals, int n) {
     for (int off = 0; off < n; off += 64) {
         int k = n - off < 64 ? n - off : 64;
         memcpy(g_hScalars, vals + off, sizeof(double) * k);
@@ -324,18 +381,7 @@ void allreduceSum(double* vals, int n) {
     }
 }
 
-int allreduceAnd(int v) {
-    double d = v ? 0.0 : 1.0;
-    allreduceSum(&d, 1);
-    return d == 0.0 ? 1 : 0;
-}
-
-void bcastHost(void* buf, size_t bytes, int root) {
-    if (g_size == 1) return;
-    if (g_socket) {
-        sock::bcastHost(buf, bytes, root);
-        return;
-    }
+void rcclBcast(void* buf, size_t bytes, int root) {
     char* p = (char*)buf;
     const size_t cap = sizeof(double) * 64;
     for (size_t off = 0; off < bytes; off += cap) {
@@ -348,13 +394,38 @@ void bcastHost(void* buf, size_t bytes, int root) {
         memcpy(p + off, g_hScalars, k);
     }
 }
+}  // namespace
+
+void allreduceSum(double* vals, int n) {
+    if (g_size == 1) return;
+    if (g_mode == Mode::Socket || g_mode == Mode::Ipc) {
+        sock::allreduceSum(vals, n);
+        return;
+    }
+    rcclAllreduceSum(vals, n);
+}
+
+int allreduceAnd(int v) {
+    double d = v ? 0.0 : 1.0;
+    allreduceSum(&d, 1);
+    return d == 0.0 ? 1 : 0;
+}
+
+void bcastHost(void* buf, size_t bytes, int root) {
+    if (g_size == 1) return;
+    if (g_mode == Mode::Socket || g_mode == Mode::Ipc) {
+        sock::bcastHost(buf, bytes, root);
+        return;
+    }
+    rcclBcast(buf, bytes, root);
+}
 
 void allgather(const void* send, void* recv, size_t bytesPerRank) {
     if (g_size == 1) {
         QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytesPerRank, hipMemcpyDeviceToDevice, S()));
         return;
     }
-    if (g_socket) {
+    if (g_mode == Mode::Socket || g_mode == Mode::Ipc) {
         const size_t all = bytesPerRank * (size_t)g_size;
         char* h = stage(bytesPerRank + all);
         QA_HIP_CHECK(hipMemcpyAsync(h, send, bytesPerRank, hipMemcpyDeviceToHost, S()));
@@ -372,9 +443,86 @@ void barrier() {
     allreduceSum(&d, 1);
 }
 
+// One-rank RCCL communicator driven through the production code paths: the
+// pipelined exchange (communication stream, ready / done events, double
+// buffering, grouped send + recv -- to itself), the staged scalar allreduce
+// and broadcast, allgather and the async-error watchdog.  A single-GPU
+// machine cannot run two RCCL ranks, so this is how those calls execute on
+// hardware before a multi-GPU job does.
+bool selfTest(std::string& report) {
+    char msg[512];
+    if (g_size != 1 || g_mode != Mode::Single) {
+        report = "self-test needs a single-process job";
+        return false;
+    }
+    if (!loadRccl()) {
+        report = "librccl could not be loaded";
+        return false;
+    }
+    ncclUniqueId id;
+    QA_NCCL(R.getUniqueId(&id), "ncclGetUniqueId");
+    QA_NCCL(R.commInitRank(&g_comm, 1, id, 0), "ncclCommInitRank");
+    g_mode = Mode::Rccl;
+    g_rank = 0;
+    createStreams();
+    bool ok = pipelined();
+    // exchange: 5 slices through 2 buffer sets, as router::multiSwap does
+    const size_t N = (size_t)1 << 20;
+    std::vector<double> host(N), back(N);
+    double *send[2], *recv[2];
+    for (int b = 0; b < 2; b++) {
+        QA_HIP_CHECK(hipMalloc(&send[b], N * sizeof(double)));
+        QA_HIP_CHECK(hipMalloc(&recv[b], N * sizeof(double)));
+    }
+    for (int s = 0; s < 5; s++) {
+        const int b = s & 1;
+        for (size_t i = 0; i < N; i++) host[i] = (double)s * 1e7 + (double)i;
+        QA_HIP_CHECK(hipMemcpyAsync(send[b], host.data(), N * sizeof(double), hipMemcpyHostToDevice, S()));
+        hipk::syncStream();  // host buffer reused next iteration
+        const Xfer x{0, send[b], recv[b], N * sizeof(double)};
+        exchangeAsync(&x, 1, b);
+        if (s > 0) exchangeWait(1 - b);
+        if (s > 0) {
+            QA_HIP_CHECK(hipMemcpyAsync(back.data(), recv[1 - b], N * sizeof(double), hipMemcpyDeviceToHost, S()));
+            hipk::syncStream();
+            for (size_t i = 0; i < N; i++) ok = ok && back[i] == (double)(s - 1) * 1e7 + (double)i;
+        }
+    }
+    exchangeWait(0);
+    QA_HIP_CHECK(hipMemcpyAsync(back.data(), recv[0], N * sizeof(double), hipMemcpyDeviceToHost, S()));
+    hipk::syncStream();
+    for (size_t i = 0; i < N; i++) ok = ok && back[i] == 4e7 + (double)i;
+    const bool exchangeOk = ok;
+    // scalars
+    double vals[70];
+    for (int i = 0; i < 70; i++) vals[i] = 0.5 * i;
+    rcclAllreduceSum(vals, 70);
+    for (int i = 0; i < 70; i++) ok = ok && vals[i] == 0.5 * i;
+    unsigned long seeds[2] = {12345ul, 678ul};
+    rcclBcast(seeds, sizeof seeds, 0);
+    ok = ok && seeds[0] == 12345ul && seeds[1] == 678ul;
+    QA_NCCL(R.allGather(send[0], recv[1], N * sizeof(double), ncclUint8, g_comm, S()), "ncclAllGather");
+    QA_HIP_CHECK(hipMemcpyAsync(back.data(), recv[1], N * sizeof(double), hipMemcpyDeviceToHost, S()));
+    hipk::syncStream();  // polls the watchdog (async errors) while waiting
+    for (size_t i = 0; i < N; i++) ok = ok && back[i] == 4e7 + (double)i;
+    watchdog(0.0);
+    int v = 0;
+    R.getVersion(&v);
+    snprintf(msg, sizeof msg, "RCCL %d (%s): pipelined exchange %s (5 slices, 2 buffer sets), allreduce, broadcast, "
+             "allgather %s", v, g_libName.c_str(), exchangeOk ? "ok" : "WRONG", ok ? "ok" : "WRONG");
+    report = msg;
+    for (int b = 0; b < 2; b++) {
+        QA_HIP_CHECK(hipFree(send[b]));
+        QA_HIP_CHECK(hipFree(recv[b]));
+    }
+    finalize();
+    return ok;
+}
+
 std::string describe() {
     if (g_size == 1) return "single process";
-    if (g_socket) return "TCP socket mesh, device buffers staged through host (QUEST_COMM=socket)";
+    if (g_mode == Mode::Socket) return "TCP socket mesh, device buffers staged through host (QUEST_COMM=socket)";
+    if (g_mode == Mode::Ipc) return ipc::describe() + " (QUEST_COMM=ipc)";
     int v = 0;
     if (R.getVersion) R.getVersion(&v);
     char buf[256];

@@ -21,8 +21,13 @@ std::string describe();            // device/backend description for reports
 const char* shortName();           // "HIP" or "CPU"
 bool stateOnHost();                // CPU build: amplitudes are host memory
 bool setTuning(const char* key, int value);  // backend knobs; false if unknown
+bool getTuning(const char* key, int* value);  // current value; false if unknown
 
 // ---- memory --------------------------------------------------------------
+// Free / total bytes of the memory the state lives in (HIP: device HBM from
+// hipMemGetInfo).  False if unknown (host build).  QUEST_DEVICE_MEM_MB
+// overrides the free amount on any build (tests of the budget check).
+bool memoryInfo(size_t* freeBytes, size_t* totalBytes);
 void allocState(QuregImpl& q);     // sets q.re / q.im (numAmpsPerChunk each)
 void freeState(QuregImpl& q);
 void* allocComm(size_t bytes);     // buffer usable by the comm transport

@@ -422,6 +422,30 @@ i64 logicalToPhysicalIndex(const QuregImpl& q, i64 idx) {
 
 }  // namespace
 
+MemoryPlan memoryPlan(int nSV, int numRanks) {
+    int g = 0;
+    while ((1 << g) < numRanks) g++;
+    const int L = nSV - g;
+    MemoryPlan m;
+    m.state = 2ll * (long long)sizeof(real) << L;
+    // multiSwap with k rank qubits: 2 (send, recv) x 2 (double buffer) x
+    // (2^k - 1) peers x slice amps x [re | im]; restoreChunks: one pair
+    const i64 partMax = (i64)1 << L;
+    for (int k = 1; k <= g; k++) {
+        i64 slice = (rt().exchangeSliceBytes >> (k - 1)) / (i64)(2 * sizeof(real));
+        slice = std::min(std::max<i64>(slice, 16), partMax >> k);
+        const long long b = 2ll * 2 * ((1ll << k) - 1) * slice * 2 * (long long)sizeof(real);
+        m.exchange = std::max(m.exchange, b);
+    }
+    if (g > 0) {
+        const i64 slice = std::min<i64>(partMax, std::max<i64>(rt().exchangeSliceBytes / (i64)(2 * sizeof(real)), 1));
+        m.exchange = std::max(m.exchange, 2ll * slice * 2 * (long long)sizeof(real));
+    }
+    m.scratch = 64ll << 20;
+    m.total = m.state + m.exchange + m.scratch;
+    return m;
+}
+
 void create(QuregImpl& q, int nSV, bool density) {
     int g = 0;
     while ((1 << g) < rt().numRanks) g++;

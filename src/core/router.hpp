@@ -20,6 +20,15 @@
 namespace qa {
 namespace router {
 
+// Device memory one rank needs for a register of nSV qubits over numRanks
+// ranks: its chunk (re + im), the largest set of exchange slice buffers a
+// distributed swap allocates (send + recv, double-buffered, per peer) and a
+// fixed allowance for reduction scratch / program upload.
+struct MemoryPlan {
+    long long state = 0, exchange = 0, scratch = 0, total = 0;
+};
+MemoryPlan memoryPlan(int nSV, int numRanks);
+
 void create(QuregImpl& q, int nSV, bool density);
 void destroy(QuregImpl& q);
 void flush(QuregImpl& q);
@@ -75,6 +84,7 @@ struct Stats {
     long long waveOps = 0, waveTransposes = 0;  // their ops / cross-lane transpositions
     long long relabels = 0;       // anti-diagonal gates on rank qubits done by relabelling chunks
     long long globalDiags = 0;    // diagonal gates on rank qubits done as per-rank scalings
+    long long flushes = 0;        // backend queue flushes (each planned into passes)
 };
 Stats& stats();
 

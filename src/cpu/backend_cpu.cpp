@@ -550,6 +550,7 @@ void enqueue(QuregImpl& q, const Op& op) {
 
 void flush(QuregImpl& q) {
     if (q.pending.empty()) return;
+    stats().flushes++;
     const size_t opsIn = q.pending.size();
     TileProgram prog;
     std::vector<Op> raw;
@@ -785,5 +786,7 @@ void hostToBuffer(const real* host, real* buf, i64 n) { memcpy(buf, host, sizeof
 namespace qa {
 namespace be {
 bool setTuning(const char*, int) { return false; }
+bool memoryInfo(size_t*, size_t*) { return false; }
+bool getTuning(const char*, int*) { return false; }
 }  // namespace be
 }  // namespace qa

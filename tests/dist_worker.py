@@ -15,6 +15,7 @@ def main():
     env = qa.Env()
     res = SCENARIOS[name](env)
     res["_ranks"] = env.num_ranks
+    res["_transport"] = qa.capi.getQuESTTransport()
     if env.rank == 0:
         import numpy as np
 

@@ -85,3 +85,40 @@ def test_restore_on_other_rank_counts(env, tmp_path, monkeypatch):
     w2 = _run("checkpoint_save", 2, ckpt2, tmp_path)
     np.testing.assert_allclose(w2, written, atol=1e-12)
     np.testing.assert_allclose(_run("checkpoint_load", 4, ckpt2, tmp_path), w2, atol=0)  # 2 -> 4
+
+
+def test_corrupt_checkpoint_leaves_state_untouched(env, tmp_path):
+    """A truncated data file, or a header whose fields are inconsistent
+    (ampsPerChunk 0, chunks x ampsPerChunk != total), is refused before the
+    register is touched (advisor finding, round 1)."""
+    import struct
+
+    import quest_amd as qa
+
+    r = qa.Register(env, 8)
+    r.init_plus()
+    r.rx(3, 0.7)
+    assert r.save(tmp_path / "ok")
+    before = r.to_numpy()
+    raw = (tmp_path / "ok.0").read_bytes()
+    # truncated: header intact, last amplitudes missing
+    (tmp_path / "trunc.0").write_bytes(raw[:-8])
+    # ampsPerChunk = 0 (offset 32) would divide by zero
+    bad = bytearray(raw)
+    bad[32:40] = struct.pack("<q", 0)
+    (tmp_path / "zero.0").write_bytes(bytes(bad))
+    # numChunks = 2 (offset 24) with ampsPerChunk = total
+    bad = bytearray(raw)
+    bad[24:28] = struct.pack("<i", 2)
+    (tmp_path / "chunks.0").write_bytes(bytes(bad))
+    s = qa.Register(env, 8)
+    s.init_classical(5)
+    for name in ("trunc", "zero", "chunks"):
+        with pytest.raises(QuESTError):
+            s.load(tmp_path / name)
+        got = s.to_numpy()
+        assert got[5] == 1 and np.count_nonzero(got) == 1, name
+    assert s.load(tmp_path / "ok")
+    np.testing.assert_array_equal(s.to_numpy(), before)
+    r.close()
+    s.close()

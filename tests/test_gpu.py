@@ -20,6 +20,35 @@ def genv():
     return e
 
 
+_KNOBS = ("tile_mode", "direct_kernels", "tile_qubits", "direct_layout", "direct_low_to_tile", "tile_wg_per_cu",
+          "wave_wg_per_cu", "fuse_blocks", "verify")
+
+
+@pytest.fixture(autouse=True)
+def restore_tuning(genv):
+    """Every test leaves the engine configuration as it found it -- the
+    build's defaults (fp64: the wave-tile engine, tile_mode 3) -- whatever
+    it changed (round 1 restored tile_mode 0 and silently ran the rest of
+    the module on the LDS kernel)."""
+    from quest_amd.ops import capi
+
+    saved = {k: capi.getQuESTTuning(k) for k in _KNOBS}
+    fusion = capi.getGateFusion()
+    yield
+    for k, v in saved.items():
+        if v is not None:
+            capi.setQuESTTuning(k, v)
+    capi.setGateFusion(fusion)
+    capi.setFusionMaxQubits(0)
+
+
+def test_wave_engine_is_the_fp64_default(genv):
+    from quest_amd.ops import capi
+
+    assert capi.getQuESTTuning("tile_mode") == 3
+    assert capi.getQuESTTuning("direct_kernels") == 1
+
+
 def test_native_hip_library_loaded(genv):
     from quest_amd.ops import capi
 
@@ -85,46 +114,48 @@ def test_random_circuit_fused_and_eager(genv, n, fusion):
     from quest_amd.utils import oracle as O
 
     qa.capi.setGateFusion(1 if fusion else 0)
-    try:
-        c = random_layered(n, 3, seed=n)
-        reg = qa.Register(genv, n)
-        reg.init_plus()
-        c.apply(reg)
-        o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
-        c.apply_oracle(o)
-        got = reg.to_numpy()
-        assert np.max(np.abs(got - o.v)) < 1e-10
-        for q in (0, n // 2, n - 1):
-            assert abs(reg.prob(q, 1) - o.prob(q, 1)) < 1e-10
-        reg.close()
-    finally:
-        qa.capi.setGateFusion(1)
+    c = random_layered(n, 3, seed=n)
+    reg = qa.Register(genv, n)
+    reg.init_plus()
+    c.apply(reg)
+    o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
+    c.apply_oracle(o)
+    got = reg.to_numpy()
+    assert np.max(np.abs(got - o.v)) < 1e-10
+    for q in (0, n // 2, n - 1):
+        assert abs(reg.prob(q, 1) - o.prob(q, 1)) < 1e-10
+    reg.close()
 
 
-@pytest.mark.parametrize("tile_mode", [0, 1, 2])
+@pytest.mark.parametrize("tile_mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("direct", [0, 1])
 def test_long_queue_every_tile_mode(genv, tile_mode, direct):
-    """More ops than one flush holds (the queue flushes itself at 256) in
-    every fused-tile variant; state must match the oracle."""
+    """More ops than one flush holds: 40 layers at 19 qubits are 1120 gates,
+    so the 1024-op backend queue flushes itself mid-circuit, in every
+    fused-tile variant (3 = the wave engine, which needs >= 19 local qubits);
+    state must match the oracle."""
     import quest_amd as qa
     from quest_amd.models import random_layered
     from quest_amd.utils import oracle as O
 
-    n = 18
+    n = 19
     assert qa.capi.setQuESTTuning("tile_mode", tile_mode) == 1
     assert qa.capi.setQuESTTuning("direct_kernels", direct) == 1
-    try:
-        c = random_layered(n, 16, seed=tile_mode * 2 + direct)
-        reg = qa.Register(genv, n)
-        reg.init_plus()
-        c.apply(reg)
-        o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
-        c.apply_oracle(o)
-        assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
-        reg.close()
-    finally:
-        qa.capi.setQuESTTuning("tile_mode", 0)
-        qa.capi.setQuESTTuning("direct_kernels", 1)
+    c = random_layered(n, 40, seed=tile_mode * 2 + direct)
+    assert len(c.gates) > 1024
+    reg = qa.Register(genv, n)
+    reg.init_plus()
+    qa.capi.resetQuESTStats()
+    c.apply(reg)
+    reg.sync()
+    st = qa.capi.getQuESTStats()
+    assert st["flushes"] >= 2, st
+    if tile_mode == 3:
+        assert st["wavePasses"] > 0, st
+    o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
+    c.apply_oracle(o)
+    assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
+    reg.close()
 
 
 def test_reductions_and_collapse_large(genv):
@@ -232,13 +263,21 @@ def test_reference_golden_suite_on_gpu(genv):
     assert passed >= 770
 
 
-@pytest.mark.parametrize("ranks,slice_kb", [(2, ""), (4, ""), (4, "1")])
-@pytest.mark.parametrize("name", ["random_ops_statevector", "random_ops_density", "measurement_and_collapse",
-                                  "calculations", "qasm_log", "rank_qubit_gates"])
-def test_distributed_equivalence_on_gpu(genv, tmp_path, name, ranks, slice_kb):
+_DIST = ["random_ops_statevector", "random_ops_density", "measurement_and_collapse", "calculations", "qasm_log",
+         "rank_qubit_gates"]
+
+
+@pytest.mark.parametrize("transport,ranks,slice_kb", [("ipc", 2, ""), ("ipc", 4, ""), ("ipc", 4, "1"),
+                                                      ("ipc-hostsync", 2, "1"), ("socket", 2, "")])
+@pytest.mark.parametrize("name", _DIST)
+def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, slice_kb):
     """The distributed router with the HIP kernels (pack/unpack, chunk
-    predicates, reductions + allreduce) on ONE GPU shared by 2 / 4 ranks over
-    the QUEST_COMM=socket test transport, against the single-rank HIP run;
+    predicates, reductions + allreduce) on ONE GPU shared by 2 / 4 ranks,
+    against the single-rank HIP run.  QUEST_COMM=ipc moves the slices
+    GPU-to-GPU-buffer through HIP IPC on the communication stream with the
+    RCCL transport's event protocol (pack / exchange / unpack overlapped,
+    double-buffered); ipc-hostsync is the same with host synchronisation
+    instead of interprocess events; socket stages through the host.
     slice_kb=1 splits every swap into many double-buffered slices."""
     import sys
 
@@ -250,15 +289,19 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, ranks, slice_kb):
 
     want = SCENARIOS[name](genv)
     out = str(tmp_path / f"{name}_{ranks}.npz")
-    res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks,
-                      env_extra={"QUEST_BACKEND": "hip", "QUEST_COMM": "socket",
-                                 "PYTHONPATH": os.path.dirname(here),
-                                 **({"QUEST_EXCHANGE_SLICE_KB": slice_kb} if slice_kb else {})}, timeout=600)
+    extra = {"QUEST_BACKEND": "hip", "QUEST_COMM": transport.split("-")[0], "PYTHONPATH": os.path.dirname(here),
+             "QUEST_COMM_TIMEOUT": "100"}
+    if transport == "ipc-hostsync":
+        extra["QUEST_IPC_EVENTS"] = "0"
+    if slice_kb:
+        extra["QUEST_EXCHANGE_SLICE_KB"] = slice_kb
+    res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks, env_extra=extra, timeout=110)
     for r, p in enumerate(res):
         assert p.returncode == 0, f"rank {r}:\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
     with np.load(out, allow_pickle=False) as z:
         got = {k: z[k] for k in z.files}
     assert int(got["_ranks"]) == ranks
+    assert ("IPC" if transport.startswith("ipc") else "socket") in str(got["_transport"])
     for k, v in want.items():
         if isinstance(v, str):
             assert str(got[k]) == v, k
@@ -277,7 +320,11 @@ def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     r = qa.Register(genv, 30)
     r.init_zero()
+    qa.capi.resetQuESTStats()
     fork_circuit().apply(r)
+    r.sync()
+    st = qa.capi.getQuESTStats()
+    assert st["wavePasses"] > 0 and st["wavePasses"] >= st["passes"] // 2, st  # the default engine ran it
     probs = [r.prob(i, 1) for i in range(30)]
     amps = [r.amp(i) for i in range(10)]
     want_p = [float(l.split(":")[1]) for l in open(os.path.join(here, "data", "fork_circuit_probs_cpu.dat"))
@@ -302,23 +349,18 @@ def test_direct_kernel_variants(genv, layout, low_to_tile):
     qa.capi.setGateFusion(0)
     qa.capi.setQuESTTuning("direct_layout", layout)
     qa.capi.setQuESTTuning("direct_low_to_tile", low_to_tile)
-    try:
-        rng = np.random.default_rng(10 * layout + low_to_tile)
-        reg = qa.Register(genv, 16)
-        o = oracle_for(reg, rng)
-        apply_random_ops(reg, o, rng, 120)
-        for t in range(16):  # every target, incl. the in-vector ones
-            apply_random_ops(reg, o, rng, 0)
-            reg.h(t)
-            o.apply(np.array([[1, 1], [1, -1]]) / np.sqrt(2), t)
-            reg.t(t)
-            o.apply(np.diag([1, np.exp(1j * np.pi / 4)]), t)
-        assert_close(reg, o)
-        reg.close()
-    finally:
-        qa.capi.setGateFusion(1)
-        qa.capi.setQuESTTuning("direct_layout", 1)
-        qa.capi.setQuESTTuning("direct_low_to_tile", 1)
+    rng = np.random.default_rng(10 * layout + low_to_tile)
+    reg = qa.Register(genv, 16)
+    o = oracle_for(reg, rng)
+    apply_random_ops(reg, o, rng, 120)
+    for t in range(16):  # every target, incl. the in-vector ones
+        apply_random_ops(reg, o, rng, 0)
+        reg.h(t)
+        o.apply(np.array([[1, 1], [1, -1]]) / np.sqrt(2), t)
+        reg.t(t)
+        o.apply(np.diag([1, np.exp(1j * np.pi / 4)]), t)
+    assert_close(reg, o)
+    reg.close()
 
 
 def test_tile_qubits_12_matches_oracle(genv):
@@ -328,18 +370,16 @@ def test_tile_qubits_12_matches_oracle(genv):
     from quest_amd.utils import oracle as O
 
     qa.capi.setQuESTTuning("tile_qubits", 12)
-    try:
-        n = 20
-        c = random_layered(n, 8, seed=12)
-        reg = qa.Register(genv, n)
-        reg.init_plus()
-        c.apply(reg)
-        o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
-        c.apply_oracle(o)
-        assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
-        reg.close()
-    finally:
-        qa.capi.setQuESTTuning("tile_qubits", 0)
+    qa.capi.setQuESTTuning("tile_mode", 0)
+    n = 20
+    c = random_layered(n, 8, seed=12)
+    reg = qa.Register(genv, n)
+    reg.init_plus()
+    c.apply(reg)
+    o = O.StateVector(n, np.full(1 << n, 1 / math.sqrt(1 << n)))
+    c.apply_oracle(o)
+    assert np.max(np.abs(reg.to_numpy() - o.v)) < 1e-10
+    reg.close()
 
 
 def test_reference_golden_suite_fp32_on_gpu():
