@@ -18,10 +18,9 @@ namespace ipc {
 namespace {
 
 int g_rank = 0, g_size = 1;
-bool g_events = true;  // GPU-side waits on interprocess events (QUEST_IPC_EVENTS=0: host sync)
-hipEvent_t g_ready[2] = {nullptr, nullptr};    // ours, interprocess
-hipEvent_t g_drained[2] = {nullptr, nullptr};
-std::vector<hipEvent_t> g_peerReady, g_peerDrained;  // [peer * 2 + slot], opened from peers' handles
+hipEvent_t g_packed[2] = {nullptr, nullptr};  // behind the packs of a slot (producer stream)
+hipEvent_t g_copied[2] = {nullptr, nullptr};  // behind the pulls of a slot (transfer stream)
+std::vector<int> g_pending[2];                // peers awaiting step 4 of a slot
 
 // send buffers we have exported (base allocation -> IPC handle, id)
 struct Exported {
@@ -32,6 +31,8 @@ struct Exported {
 };
 std::vector<Exported> g_exported;
 unsigned long long g_nextId = 1;
+unsigned long long g_generation = 0;          // our frees of exported buffers
+std::vector<unsigned long long> g_peerGeneration;  // last generation seen from each peer
 
 // peers' send buffers we have opened
 struct Imported {
@@ -42,17 +43,16 @@ struct Imported {
 };
 std::vector<Imported> g_imported;
 unsigned long long g_clock = 0;
+unsigned long long g_exchanges = 0;
 constexpr size_t kMaxImportedPerPeer = 16;
 
 struct Token {
+    unsigned long long generation;  // buffers the sender has freed so far
     unsigned long long id;
     hipIpcMemHandle_t handle;
     unsigned long long offset, bytes;
 };
 
-struct EventHandles {
-    hipIpcEventHandle_t ready[2], drained[2];
-};
 
 const Exported& exportBuffer(const void* p) {
     const char* c = static_cast<const char*>(p);
@@ -72,6 +72,23 @@ const Exported& exportBuffer(const void* p) {
 
 char* importBuffer(int peer, const Token& t) {
     g_clock++;
+    if (t.generation != g_peerGeneration[(size_t)peer]) {
+        // the peer freed buffers since we last looked: drop every mapping of
+        // its memory.  (A new allocation can reuse the freed range, and
+        // re-opening it while the old mapping is open hands back the old
+        // mapping with the old size: hipMemcpyAsync then rejects copies that
+        // are longer than that with hipErrorInvalidValue.)
+        QA_HIP_CHECK(hipDeviceSynchronize());
+        for (size_t i = 0; i < g_imported.size();) {
+            if (g_imported[i].peer == peer) {
+                QA_HIP_CHECK(hipIpcCloseMemHandle(g_imported[i].ptr));
+                g_imported.erase(g_imported.begin() + (long)i);
+            } else {
+                i++;
+            }
+        }
+        g_peerGeneration[(size_t)peer] = t.generation;
+    }
     size_t mine = 0, lru = (size_t)-1;
     for (size_t i = 0; i < g_imported.size(); i++) {
         Imported& m = g_imported[i];
@@ -101,26 +118,11 @@ char* importBuffer(int peer, const Token& t) {
 void init(int rank, int size) {
     g_rank = rank;
     g_size = size;
-    const char* e = getenv("QUEST_IPC_EVENTS");
-    g_events = !(e && atoi(e) == 0);
-    if (!g_events) return;
-    EventHandles mine;
+    g_peerGeneration.assign((size_t)size, 0);
     for (int s = 0; s < 2; s++) {
-        QA_HIP_CHECK(hipEventCreateWithFlags(&g_ready[s], hipEventInterprocess | hipEventDisableTiming));
-        QA_HIP_CHECK(hipEventCreateWithFlags(&g_drained[s], hipEventInterprocess | hipEventDisableTiming));
-        QA_HIP_CHECK(hipIpcGetEventHandle(&mine.ready[s], g_ready[s]));
-        QA_HIP_CHECK(hipIpcGetEventHandle(&mine.drained[s], g_drained[s]));
-    }
-    std::vector<EventHandles> all((size_t)size);
-    sock::allgatherHost(&mine, all.data(), sizeof(EventHandles));
-    g_peerReady.assign((size_t)size * 2, nullptr);
-    g_peerDrained.assign((size_t)size * 2, nullptr);
-    for (int p = 0; p < size; p++) {
-        if (p == rank) continue;
-        for (int s = 0; s < 2; s++) {
-            QA_HIP_CHECK(hipIpcOpenEventHandle(&g_peerReady[(size_t)p * 2 + s], all[(size_t)p].ready[s]));
-            QA_HIP_CHECK(hipIpcOpenEventHandle(&g_peerDrained[(size_t)p * 2 + s], all[(size_t)p].drained[s]));
-        }
+        QA_HIP_CHECK(hipEventCreateWithFlags(&g_packed[s], hipEventDisableTiming));
+        QA_HIP_CHECK(hipEventCreateWithFlags(&g_copied[s], hipEventDisableTiming));
+        g_pending[s].clear();
     }
 }
 
@@ -129,32 +131,39 @@ void finalize() {
     for (Imported& m : g_imported) (void)hipIpcCloseMemHandle(m.ptr);
     g_imported.clear();
     g_exported.clear();
-    for (hipEvent_t& ev : g_peerReady)
-        if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t& ev : g_peerDrained)
-        if (ev) (void)hipEventDestroy(ev);
-    g_peerReady.clear();
-    g_peerDrained.clear();
     for (int s = 0; s < 2; s++) {
-        if (g_ready[s]) (void)hipEventDestroy(g_ready[s]);
-        if (g_drained[s]) (void)hipEventDestroy(g_drained[s]);
-        g_ready[s] = g_drained[s] = nullptr;
+        if (g_packed[s]) (void)hipEventDestroy(g_packed[s]);
+        if (g_copied[s]) (void)hipEventDestroy(g_copied[s]);
+        g_packed[s] = g_copied[s] = nullptr;
+        g_pending[s].clear();
     }
     g_size = 1;
 }
 
+void complete(int slot) {
+    slot &= 1;
+    if (g_pending[slot].empty()) return;
+    hipk::syncStream(g_copied[slot]);
+    for (int peer : g_pending[slot]) {
+        int a = 1, b = 0;
+        sock::sendrecv(peer, &a, &b, sizeof a);
+    }
+    g_pending[slot].clear();
+}
+
 void transfer(const comm::Xfer* x, int n, int slot, hipStream_t producer, hipStream_t stream) {
     slot &= 1;
-    // 1. our send buffers are complete once the producer reaches this point
-    if (g_events)
-        QA_HIP_CHECK(hipEventRecord(g_ready[slot], producer));
-    else
-        QA_HIP_CHECK(hipStreamSynchronize(producer));
+    g_exchanges++;
+    complete(slot);  // the previous exchange of this slot, if the caller did not wait for it
+    // 1. our send buffers are complete
+    QA_HIP_CHECK(hipEventRecord(g_packed[slot], producer));
+    hipk::syncStream(g_packed[slot]);
     // 2. tell each peer where its data is, learn where ours is
     std::vector<Token> mine((size_t)n), theirs((size_t)n);
     for (int i = 0; i < n; i++) {
         const Exported& e = exportBuffer(x[i].send);
         memset(&mine[(size_t)i], 0, sizeof(Token));
+        mine[(size_t)i].generation = g_generation;
         mine[(size_t)i].id = e.id;
         mine[(size_t)i].handle = e.handle;
         mine[(size_t)i].offset = (unsigned long long)(static_cast<const char*>(x[i].send) - e.base);
@@ -169,23 +178,17 @@ void transfer(const comm::Xfer* x, int n, int slot, hipStream_t producer, hipStr
                     x[i].bytes, x[i].peer, t.bytes);
             exit(EXIT_FAILURE);
         }
-        char* src = importBuffer(x[i].peer, t) + t.offset;
-        if (g_events) QA_HIP_CHECK(hipStreamWaitEvent(stream, g_peerReady[(size_t)x[i].peer * 2 + slot], 0));
-        QA_HIP_CHECK(hipMemcpyAsync(x[i].recv, src, x[i].bytes, hipMemcpyDeviceToDevice, stream));
+        const char* src = importBuffer(x[i].peer, t) + t.offset;
+        const hipError_t e = hipMemcpyAsync(x[i].recv, src, x[i].bytes, hipMemcpyDeviceToDevice, stream);
+        if (e != hipSuccess) {
+            fprintf(stderr, "QuEST ipc: rank %d exchange %llu: copy of %zu B from rank %d (buffer id %llu + %llu) "
+                            "failed: %s\n",
+                    g_rank, g_exchanges, x[i].bytes, x[i].peer, t.id, t.offset, hipGetErrorString(e));
+            exit(EXIT_FAILURE);
+        }
+        g_pending[slot].push_back(x[i].peer);
     }
-    // 4./5. we are done reading the peers' buffers
-    if (g_events)
-        QA_HIP_CHECK(hipEventRecord(g_drained[slot], stream));
-    else
-        QA_HIP_CHECK(hipStreamSynchronize(stream));
-    for (int i = 0; i < n; i++) {
-        int a = 1, b = 0;
-        sock::sendrecv(x[i].peer, &a, &b, sizeof a);
-    }
-    // 6. and so are they with ours
-    if (g_events)
-        for (int i = 0; i < n; i++)
-            QA_HIP_CHECK(hipStreamWaitEvent(stream, g_peerDrained[(size_t)x[i].peer * 2 + slot], 0));
+    QA_HIP_CHECK(hipEventRecord(g_copied[slot], stream));
 }
 
 void forget(const void* p) {
@@ -193,14 +196,12 @@ void forget(const void* p) {
     for (size_t i = 0; i < g_exported.size(); i++)
         if (c >= g_exported[i].base && c < g_exported[i].base + g_exported[i].size) {
             g_exported.erase(g_exported.begin() + (long)i);
+            g_generation++;
             return;
         }
 }
 
-std::string describe() {
-    return g_events ? "HIP IPC on one device (interprocess events, GPU-side waits)"
-                    : "HIP IPC on one device (host-synchronised, QUEST_IPC_EVENTS=0)";
-}
+std::string describe() { return "HIP IPC between ranks on one device"; }
 
 }  // namespace ipc
 }  // namespace qa

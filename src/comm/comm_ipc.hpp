@@ -10,24 +10,25 @@
 // comm_socket.cpp.
 //
 // Protocol of one exchange with peers x[0..n) (buffers from allocComm):
-//   1. the producer stream records this rank's interprocess event READY[slot]
-//      (its send buffers are packed once that event fires);
+//   1. a local event recorded on the producer stream behind the packs; the
+//      host waits for it (the send buffers of this slot are complete);
 //   2. token round 1 (socket, pairwise in the router's (peer ^ rank) order):
 //      every rank tells each peer where the send buffer meant for it lives
 //      (allocation id + IPC memory handle + offset + bytes);
-//   3. the transfer stream waits on the peer's READY[slot] and copies the
-//      peer's send buffer into this rank's receive buffer (a pull);
-//   4. the transfer stream records DRAINED[slot] (this rank has finished
-//      reading every peer's send buffer);
-//   5. token round 2: "DRAINED recorded";
-//   6. the transfer stream waits on every peer's DRAINED[slot], so whoever
-//      waits on the transfer stream afterwards knows both that the data has
-//      arrived and that its own send buffers are free again.
-// Every wait is a GPU-side wait on an event the peer recorded BEFORE it sent
-// the token that let us issue the wait, so no rank ever waits on a record
-// that has not been issued.  QUEST_IPC_EVENTS=0 replaces the GPU-side waits
-// by host synchronisation before each token (slower, no interprocess
-// events needed).
+//   3. the transfer stream copies each peer's send buffer into this rank's
+//      receive buffer (a pull through the IPC mapping) and records a local
+//      "copied" event -- transfer() returns here, the copies run while the
+//      compute stream goes on unpacking / packing other slices;
+//   4. complete(slot), called when the compute stream is about to depend on
+//      the slot (comm::exchangeWait) or before the slot is reused: the host
+//      waits for the "copied" event, then token round 2 tells the peers that
+//      their send buffers are free again.
+// No rank ever copies from a buffer its owner has not finished (step 1
+// precedes the token), and no rank repacks a send buffer before every reader
+// has confirmed its copy (step 4 precedes the next use of the slot).  All
+// waits are on local events; interprocess events (whose stream waits failed
+// intermittently on ROCm 7.2 with hipErrorInvalidValue on the following copy)
+// are not needed.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -37,12 +38,14 @@
 namespace qa {
 namespace ipc {
 
-// Collective: socket control mesh (already up), interprocess events.
+// After the socket control mesh is up (comm_socket.cpp).
 void init(int rank, int size);
 void finalize();
-// One exchange as above; `producer` is the stream that packs the send
+// Steps 1-3 of one exchange; `producer` is the stream that packs the send
 // buffers, `stream` the one the copies run on (may be the same).
 void transfer(const comm::Xfer* x, int n, int slot, hipStream_t producer, hipStream_t stream);
+// Step 4 for the exchange last issued with `slot` (no-op if none pending).
+void complete(int slot);
 // A comm buffer is about to be freed: forget its handle (a later allocation
 // at the same address gets a new id, so peers re-open it).
 void forget(const void* p);

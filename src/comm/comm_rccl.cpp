@@ -301,6 +301,7 @@ namespace {
 void deviceExchange(const Xfer* x, int n, int slot, hipStream_t producer, hipStream_t stream) {
     if (g_mode == Mode::Ipc) {
         ipc::transfer(x, n, slot, producer, stream);
+        if (stream == producer) ipc::complete(slot);  // not pipelined: done on return
         return;
     }
     QA_NCCL(R.groupStart(), "ncclGroupStart");
@@ -364,6 +365,7 @@ void exchangeAsync(const Xfer* x, int n, int slot) {
 
 void exchangeWait(int slot) {
     if (!pipelined()) return;
+    if (g_mode == Mode::Ipc) ipc::complete(slot);
     QA_HIP_CHECK(hipStreamWaitEvent(S(), g_done[slot & 1], 0));
 }
 

@@ -268,7 +268,7 @@ _DIST = ["random_ops_statevector", "random_ops_density", "measurement_and_collap
 
 
 @pytest.mark.parametrize("transport,ranks,slice_kb", [("ipc", 2, ""), ("ipc", 4, ""), ("ipc", 4, "1"),
-                                                      ("ipc-hostsync", 2, "1"), ("socket", 2, "")])
+                                                      ("ipc-nopipe", 2, "1"), ("socket", 2, "")])
 @pytest.mark.parametrize("name", _DIST)
 def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, slice_kb):
     """The distributed router with the HIP kernels (pack/unpack, chunk
@@ -276,8 +276,8 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     against the single-rank HIP run.  QUEST_COMM=ipc moves the slices
     GPU-to-GPU-buffer through HIP IPC on the communication stream with the
     RCCL transport's event protocol (pack / exchange / unpack overlapped,
-    double-buffered); ipc-hostsync is the same with host synchronisation
-    instead of interprocess events; socket stages through the host.
+    double-buffered); ipc-nopipe runs every exchange on the compute stream
+    (QUEST_EXCHANGE_PIPELINE=0); socket stages through the host.
     slice_kb=1 splits every swap into many double-buffered slices."""
     import sys
 
@@ -291,8 +291,8 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     out = str(tmp_path / f"{name}_{ranks}.npz")
     extra = {"QUEST_BACKEND": "hip", "QUEST_COMM": transport.split("-")[0], "PYTHONPATH": os.path.dirname(here),
              "QUEST_COMM_TIMEOUT": "100"}
-    if transport == "ipc-hostsync":
-        extra["QUEST_IPC_EVENTS"] = "0"
+    if transport == "ipc-nopipe":
+        extra["QUEST_EXCHANGE_PIPELINE"] = "0"
     if slice_kb:
         extra["QUEST_EXCHANGE_SLICE_KB"] = slice_kb
     res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks, env_extra=extra, timeout=110)

@@ -1,27 +1,19 @@
-#!/usr/bin/env bash
-# Run GPU steps in order, each under its own time limit; a step that ends in
-# a fault-like way (timeout 124/137, abort 134, segfault 139, or a signal)
-# stops the whole sequence, an ordinary failure (e.g. pytest exit 1) does not.
-#
-# usage: tools/gpu_steps.sh "<seconds>|<name>|<command>" ...
-# output of each step -> gpurun_out/<name>.log ; summary -> gpurun_out/steps.txt
+#!/bin/bash
+# Run GPU steps one after another under their own time limits; a step that
+# ends with a test failure (exit 1) lets the next one run, anything else
+# (timeout 124/137, abort 134, segfault 139, ...) ends the script there.
+#   tools/gpu_steps.sh "<name>|<seconds>|<command>" ...
 mkdir -p gpurun_out
-: > gpurun_out/steps.txt
 for spec in "$@"; do
-    secs="${spec%%|*}"
-    rest="${spec#*|}"
-    name="${rest%%|*}"
-    cmd="${rest#*|}"
-    echo "=== $name ($secs s): $cmd" | tee -a gpurun_out/steps.txt
+    name=${spec%%|*}; rest=${spec#*|}; secs=${rest%%|*}; cmd=${rest#*|}
+    echo "=== $name ($secs s): $cmd"
     start=$(date +%s)
     timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
     rc=$?
-    end=$(date +%s)
-    echo "=== $name rc=$rc time=$((end - start))s" | tee -a gpurun_out/steps.txt
+    echo "=== $name rc=$rc $(( $(date +%s) - start )) s"
     tail -5 "gpurun_out/$name.log"
-    case $rc in
-        0|1|2|3|4|5) ;;
-        *) echo "stopping after fault-like exit $rc" | tee -a gpurun_out/steps.txt; exit $rc ;;
-    esac
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+        echo "=== stopping after $name (rc=$rc)"
+        exit $rc
+    fi
 done
-exit 0
