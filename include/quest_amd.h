@@ -103,6 +103,7 @@ typedef struct QuESTStats {
     long long relabels;       /* X/Y-like gates on rank qubits applied by relabelling chunks (no data moved) */
     long long globalDiags;    /* diagonal one-qubit gates on rank qubits applied as per-rank scalings */
     long long flushes;        /* backend queue flushes (each planned into fused passes) */
+    long long marginalPasses; /* one-pass computations of every qubit's marginal (calcProbOfOutcome cache) */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

@@ -979,6 +979,7 @@ void copyChunkFromBuffers(Qureg qureg, const qreal* re, const qreal* im) {
     be::flush(q);
     router::canonicalise(q);
     be::fromBuffer(q, 0, q.numAmpsPerChunk, re, im);
+    router::touch(q);
     be::deviceSync();
 }
 
@@ -1026,6 +1027,7 @@ void getQuESTStats(QuESTStats* s) {
     s->relabels = stats().relabels;
     s->globalDiags = stats().globalDiags;
     s->flushes = stats().flushes;
+    s->marginalPasses = stats().marginalPasses;
 }
 
 void resetQuESTStats(void) { stats() = Stats(); }

@@ -52,6 +52,9 @@ void copyState(QuregImpl& dst, QuregImpl& src);
 // ---- reductions (partials of this chunk) -----------------------------------
 // sum |amp|^2 over amplitudes whose physical bit `bit` == bitVal (bit < 0: all)
 double sumSq(QuregImpl& q, int bit, int bitVal);
+// every local bit at once (one pass): zeroSums[b] = sumSq(q, b, 0) for b < q.L,
+// *total = sumSq(q, -1, 0)
+void marginals(QuregImpl& q, double* zeroSums, double* total);
 // sum conj(bra) * ket
 void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]);
 // Density-matrix diagonal: sum over logical row r in [0, 2^n) of Re rho(r,r),

@@ -79,6 +79,14 @@ struct QuregImpl {
     std::vector<Op> lpending; // distributed registers: ops in LOGICAL qubits awaiting routing
     bool jointAlloc = false;  // HIP: re and im share one allocation (freed through re)
     void* be = nullptr;       // backend-private state
+    // Router-level change counter of the LOGICAL state (bumped identically on
+    // every rank by every op / overwrite) and the one-qubit marginals cached
+    // at margGen: margP0[lg] = sum |a|^2 over amplitudes with logical qubit lg
+    // = 0 (all ranks), margP0[nSV] = the norm.
+    u64 stateGen = 0;
+    u64 margGen = ~0ull;
+    u64 probGen = ~0ull;      // state generation of the last single-qubit query
+    double margP0[65];
     real* hostRe = nullptr;   // optional host mirror (Qureg.stateVec)
     real* hostIm = nullptr;
     bool permIdentity() const {

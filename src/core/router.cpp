@@ -389,6 +389,7 @@ constexpr size_t kLogicalWindow = 1024;
 
 // Accept a logical op: single-rank registers go straight to the backend.
 void submit(QuregImpl& q, const Op& lop) {
+    q.stateGen++;
     if (!distributed(q)) {
         issue(q, lop);
         return;
@@ -405,6 +406,7 @@ void drain(QuregImpl& q) {
 
 // Identity qubit layout and chunk placement (callers overwrite the state).
 void resetLayout(QuregImpl& q) {
+    q.stateGen++;
     for (int i = 0; i < 64; i++) {
         q.l2p[i] = q.p2l[i] = i;
         q.lastUse[i] = 0;
@@ -524,6 +526,7 @@ void densChan2(QuregImpl& q, int r1, int r2, int c1, int c2, real offFac, real k
 }
 
 void collapse(QuregImpl& q, int qubit, int outcome, real renorm) {
+    q.stateGen++;
     flushLogical(q);
     int p = q.l2p[qubit];
     if (p >= q.L) {
@@ -547,6 +550,7 @@ void collapse(QuregImpl& q, int qubit, int outcome, real renorm) {
 }
 
 void densCollapse(QuregImpl& q, int qubit, int outcome, real prob) {
+    q.stateGen++;
     // keep elements whose row bit (qubit) and column bit (qubit + n) both equal
     // the outcome; scale them by 1/prob (reference divides by p, not sqrt(p))
     flushLogical(q);
@@ -629,6 +633,7 @@ void initSingleQubit(QuregImpl& q, int qubit, int outcome, real val) {
 }
 
 void setAmps(QuregImpl& q, i64 start, const real* re, const real* im, i64 n) {
+    q.stateGen++;
     if (n == q.numAmpsTotal && start == 0) {
         drain(q);
         resetLayout(q);
@@ -644,6 +649,7 @@ void clone(QuregImpl& dst, QuregImpl& src) {
     drain(src);
     drain(dst);
     be::copyState(dst, src);
+    dst.stateGen++;
     memcpy(dst.l2p, src.l2p, sizeof dst.l2p);
     memcpy(dst.p2l, src.p2l, sizeof dst.p2l);
     memcpy(dst.lastUse, src.lastUse, sizeof dst.lastUse);
@@ -688,6 +694,7 @@ void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
         canonicalise(b);
     }
     be::axpby(a, alpha, b, beta);
+    a.stateGen++;
 }
 
 void canonicalise(QuregImpl& q) {
@@ -765,9 +772,39 @@ static double allSum(double x) {
     return x;
 }
 
+// P(qubit = 0) times the norm.  The first query after a state change reads
+// the half of the state it needs; a second query of the same state computes
+// every qubit's marginal in one pass (be::marginals, one allreduce of nSV + 1
+// values) and later queries are answered from that cache until the next
+// change.  Programs that read all marginals back to back (the fork's
+// tutorial_example.c:521-525) stream the state 1.5 times instead of n / 2.
+// The decisions depend only on stateGen, which changes identically on every
+// rank, so all ranks take the same collective path.
+static bool marginalCacheOn() {
+    static const bool off = getenv("QUEST_MARGINAL_CACHE") && atoi(getenv("QUEST_MARGINAL_CACHE")) == 0;
+    return !off;
+}
+
 double probZero(QuregImpl& q, int qubit) {
     drain(q);
+    if (marginalCacheOn() && q.margGen == q.stateGen) return q.margP0[qubit];
     stats().reductions++;
+    if (marginalCacheOn() && q.probGen == q.stateGen) {
+        double z[65], tot;
+        be::marginals(q, z, &tot);
+        double v[65];
+        for (int lg = 0; lg < q.nSV; lg++) {
+            const int p = q.l2p[lg];
+            v[lg] = p < q.L ? z[p] : (chunkBit(q, p) == 0 ? tot : 0.0);
+        }
+        v[q.nSV] = tot;
+        if (comm::active()) comm::allreduceSum(v, q.nSV + 1);
+        memcpy(q.margP0, v, sizeof(double) * (size_t)(q.nSV + 1));
+        q.margGen = q.stateGen;
+        stats().marginalPasses++;
+        return q.margP0[qubit];
+    }
+    q.probGen = q.stateGen;
     int p = q.l2p[qubit];
     double part;
     if (p >= q.L)
@@ -843,6 +880,8 @@ void prepareOverwrite(QuregImpl& q) {
     drain(q);
     resetLayout(q);
 }
+
+void touch(QuregImpl& q) { q.stateGen++; }
 
 void writeChunk(QuregImpl& q, const real* re, const real* im) {
     drain(q);

@@ -60,6 +60,8 @@ void canonicalise(QuregImpl& q);
 // ---- reads and reductions (collective over ranks) -------------------------------
 cplx getAmp(QuregImpl& q, i64 flatIndex);
 double probZero(QuregImpl& q, int qubit);
+// the state was changed outside the router (e.g. copyChunkFromBuffers)
+void touch(QuregImpl& q);
 double sumSqAll(QuregImpl& q);
 double densProbZero(QuregImpl& q, int qubit);
 double densTrace(QuregImpl& q);
@@ -85,6 +87,7 @@ struct Stats {
     long long relabels = 0;       // anti-diagonal gates on rank qubits done by relabelling chunks
     long long globalDiags = 0;    // diagonal gates on rank qubits done as per-rank scalings
     long long flushes = 0;        // backend queue flushes (each planned into passes)
+    long long marginalPasses = 0; // one-pass all-qubit marginals (probZero cache fills)
 };
 Stats& stats();
 

@@ -11,6 +11,8 @@
 #include <cstring>
 #include <vector>
 
+#include <omp.h>
+
 #include "../core/backend.hpp"
 #include "../core/router.hpp"
 #include "../core/tiles.hpp"
@@ -661,6 +663,42 @@ double sumSq(QuregImpl& q, int bit, int bitVal) {
         s += (double)q.re[i] * q.re[i] + (double)q.im[i] * q.im[i];
     }
     return s;
+}
+
+// One pass over blocks of 2^12 amplitudes: bits inside a block per element,
+// bits above it from the block total.
+void marginals(QuregImpl& q, double* zeroSums, double* total) {
+    flush(q);
+    const int L = q.L, kb = std::min(L, 12);
+    const i64 blk = (i64)1 << kb, nBlk = q.numAmpsPerChunk >> kb;
+    // per-thread partials summed in thread order: deterministic
+    std::vector<double> parts;
+#pragma omp parallel if (q.numAmpsPerChunk >= kOmpMin)
+    {
+        double mine[65] = {0};
+#pragma omp single
+        parts.assign(65 * (size_t)omp_get_num_threads(), 0.0);
+#pragma omp for schedule(static)
+        for (i64 B = 0; B < nBlk; B++) {
+            double bs = 0;
+            for (i64 i = 0; i < blk; i++) {
+                const i64 k = B * blk + i;
+                const double x = (double)q.re[k] * q.re[k] + (double)q.im[k] * q.im[k];
+                bs += x;
+                for (int b = 0; b < kb; b++)
+                    if (!((i >> b) & 1)) mine[b] += x;
+            }
+            for (int b = kb; b < L; b++)
+                if (!((B >> (b - kb)) & 1)) mine[b] += bs;
+            mine[64] += bs;
+        }
+        memcpy(&parts[65 * (size_t)omp_get_thread_num()], mine, sizeof mine);
+    }
+    double acc[65] = {0};
+    for (size_t t = 0; t < parts.size(); t += 65)
+        for (int b = 0; b < 65; b++) acc[b] += parts[t + b];
+    for (int b = 0; b < L; b++) zeroSums[b] = acc[b];
+    *total = acc[64];
 }
 
 void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]) {

@@ -107,6 +107,123 @@ __global__ __launch_bounds__(kThreads) void sumSqBitKernel(const T* __restrict__
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// All one-qubit marginals in ONE pass: out[b] = sum of |a_i|^2 over i with
+// bit b == 0, for every local bit b, plus the total.  The fork's program asks
+// for P(q = 1) of all 30 qubits back to back (tutorial_example.c:521-525);
+// one sumSqBitKernel per qubit re-streams half the state each time
+// (QuEST_gpu.cu:1515-1551 streams it per call too).
+//
+// A tile of 2^m amplitudes is 256 threads x kMargUnits 16-byte units x VN
+// elements: element bits [0, vb), thread bits [vb, vb + 8), unit bits
+// [vb + 8, vb + 11), tile bits above.  Workgroup w of G = 2^g takes tiles
+// w, w + G, ...: tile bits [m, m + g) are blockIdx's (applied by the finish
+// kernel to the workgroup total), the rest vary per iteration.  Partial slots
+// per workgroup: 0 total, 1 .. vb element bits, then 8 thread bits, 3 unit
+// bits, then the varying tile bits.
+constexpr int kMargUnits = 8;
+constexpr int kMargSlots = 64;
+double* g_margPartials = nullptr;  // kMargSlots * kMaxBlocks
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void marginalsKernel(const T* __restrict__ re, const T* __restrict__ im,
+                                                            long long numTiles, int g, int nVary,
+                                                            double* __restrict__ part) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = Vec16<T>::n;
+    constexpr int VB = VN == 2 ? 1 : 2;
+    constexpr int kMaxVary = 32;
+    const int G = gridDim.x;
+    double tot = 0, ez[VB], uz[3], hz[kMaxVary];
+#pragma unroll
+    for (int e = 0; e < VB; e++) ez[e] = 0;
+#pragma unroll
+    for (int e = 0; e < 3; e++) uz[e] = 0;
+#pragma unroll
+    for (int e = 0; e < kMaxVary; e++) hz[e] = 0;
+    for (long long t = blockIdx.x; t < numTiles; t += G) {
+        const long long base = t * (kThreads * kMargUnits);   // in units
+        double s[kMargUnits];
+#pragma unroll
+        for (int k = 0; k < kMargUnits; k++) {
+            const V a = reinterpret_cast<const V*>(re)[base + k * kThreads + threadIdx.x];
+            const V b = reinterpret_cast<const V*>(im)[base + k * kThreads + threadIdx.x];
+            const T* pa = reinterpret_cast<const T*>(&a);
+            const T* pb = reinterpret_cast<const T*>(&b);
+            double x[VN];
+#pragma unroll
+            for (int e = 0; e < VN; e++) x[e] = (double)pa[e] * pa[e] + (double)pb[e] * pb[e];
+            double sk = 0;
+#pragma unroll
+            for (int e = 0; e < VN; e++) {
+                sk += x[e];
+#pragma unroll
+                for (int eb = 0; eb < VB; eb++)
+                    if (!((e >> eb) & 1)) ez[eb] += x[e];
+            }
+            s[k] = sk;
+        }
+        double st = 0;
+#pragma unroll
+        for (int k = 0; k < kMargUnits; k++) {
+            st += s[k];
+#pragma unroll
+            for (int kb = 0; kb < 3; kb++)
+                if (!((k >> kb) & 1)) uz[kb] += s[k];
+        }
+        tot += st;
+        const long long hi = t >> g;   // tile bits that vary across this workgroup's tiles
+#pragma unroll
+        for (int h = 0; h < kMaxVary; h++)
+            if (h < nVary && !((hi >> h) & 1)) hz[h] += st;
+    }
+    // block sums of every slot (thread bits: the thread's total where its bit is 0)
+    __shared__ double red[kMargSlots][kThreads / 64];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    auto put = [&](int slot, double v) {
+        v = waveSum(v);
+        if (l == 0) red[slot][w] = v;
+    };
+    int slot = 0;
+    put(slot++, tot);
+#pragma unroll
+    for (int e = 0; e < VB; e++) put(slot++, ez[e]);
+#pragma unroll
+    for (int b = 0; b < 8; b++) put(slot++, ((threadIdx.x >> b) & 1) ? 0.0 : tot);
+#pragma unroll
+    for (int e = 0; e < 3; e++) put(slot++, uz[e]);
+#pragma unroll
+    for (int h = 0; h < kMaxVary; h++)
+        if (h < nVary) put(slot++, hz[h]);
+    __syncthreads();
+    if (threadIdx.x < slot) {
+        double v = 0;
+#pragma unroll
+        for (int k = 0; k < kThreads / 64; k++) v += red[threadIdx.x][k];
+        part[(long long)threadIdx.x * kMaxBlocks + blockIdx.x] = v;
+    }
+}
+
+// out[b] for b < L (zero-bit sums), out[L] = total, from the per-workgroup slots
+__global__ __launch_bounds__(kThreads) void marginalsFinishKernel(const double* __restrict__ part, int G, int g,
+                                                                  int vb, int L, double* __restrict__ out) {
+    const int m = vb + 11;
+    for (int b = 0; b <= L; b++) {
+        double acc = 0;
+        if (b == L) {
+            for (int i = threadIdx.x; i < G; i += blockDim.x) acc += part[i];
+        } else if (b >= m && b < m + g) {   // workgroup-index bits: totals of the workgroups with the bit clear
+            for (int i = threadIdx.x; i < G; i += blockDim.x)
+                if (!((i >> (b - m)) & 1)) acc += part[i];
+        } else {
+            const int slot = b < m ? 1 + b : 1 + m + (b - m - g);
+            for (int i = threadIdx.x; i < G; i += blockDim.x) acc += part[(long long)slot * kMaxBlocks + i];
+        }
+        const double s = blockSum(acc);
+        if (threadIdx.x == 0) out[b] = s;
+        __syncthreads();
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void innerKernel(const T* __restrict__ ar, const T* __restrict__ ai,
                                                         const T* __restrict__ br, const T* __restrict__ bi,
@@ -271,6 +388,44 @@ double reduceSumSq(const real* re, const real* im, i64 n, int bit, int bitVal) {
     double r;
     finish(nb, 1, &r);
     return r;
+}
+
+void reduceMarginals(const real* re, const real* im, int L, double* zeroSums, double* total) {
+    ensureScratch();
+    constexpr int VN = Vec16<real>::n;
+    constexpr int vb = VN == 2 ? 1 : 2;
+    const int m = vb + 11;
+    if (L < m) {   // small chunk: one bit at a time (tiny launches)
+        for (int b = 0; b < L; b++) zeroSums[b] = reduceSumSq(re, im, 1ll << L, b, 0);
+        *total = reduceSumSq(re, im, 1ll << L, -1, 0);
+        return;
+    }
+    static double* dOut = nullptr;
+    static double* hOut = nullptr;
+    if (!g_margPartials) {
+        QA_HIP_CHECK(hipMalloc(&g_margPartials, sizeof(double) * kMargSlots * kMaxBlocks));
+        QA_HIP_CHECK(hipMalloc(&dOut, sizeof(double) * 64));
+        QA_HIP_CHECK(hipHostMalloc(&hOut, sizeof(double) * 64, hipHostMallocDefault));
+    }
+    const int tileBits = L - m;
+    int g = 0;
+    while (g < tileBits && (2 << g) <= kMaxBlocks) g++;
+    const int nVary = tileBits - g;
+    if (nVary > 32 || 1 + vb + 11 + nVary > kMargSlots) {
+        fprintf(stderr, "QuEST: marginals of %d local qubits exceed the kernel's slots\n", L);
+        exit(EXIT_FAILURE);
+    }
+    const long long numTiles = 1ll << tileBits;
+    hipLaunchKernelGGL(marginalsKernel<real>, dim3(1 << g), dim3(kThreads), 0, stream(), re, im, numTiles, g, nVary,
+                       g_margPartials);
+    QA_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(marginalsFinishKernel, dim3(1), dim3(kThreads), 0, stream(), g_margPartials, 1 << g, g, vb, L,
+                       dOut);
+    QA_HIP_CHECK(hipGetLastError());
+    QA_HIP_CHECK(hipMemcpyAsync(hOut, dOut, sizeof(double) * (L + 1), hipMemcpyDeviceToHost, stream()));
+    syncStream();
+    for (int b = 0; b < L; b++) zeroSums[b] = hOut[b];
+    *total = hOut[L];
 }
 
 void reduceInner(const real* ar, const real* ai, const real* br, const real* bi, i64 n, double out[2]) {

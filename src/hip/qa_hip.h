@@ -137,6 +137,8 @@ void launchDensInitPure(real* re, real* im, i64 n, const real* pr, const real* p
 
 // reductions: results are written to `out` (device, doubles) and copied back
 double reduceSumSq(const real* re, const real* im, i64 n, int bit, int bitVal);
+// zeroSums[b] = sum |a_i|^2 over i with bit b clear (b < L), *total = sum |a_i|^2, one pass
+void reduceMarginals(const real* re, const real* im, int L, double* zeroSums, double* total);
 void reduceInner(const real* ar, const real* ai, const real* br, const real* bi, i64 n, double out[2]);
 double reduceMaxDiff(const real* ar, const real* ai, const real* br, const real* bi, i64 n);
 double reduceDensDiag(const real* re, i64 chunkAmps, const u64* offs, int nq, int skipBit, i64 chunkStart);

@@ -102,3 +102,26 @@ def test_rccl_transport_self_test(genv):
     assert ok, report
     assert "RCCL" in report and "WRONG" not in report, report
     print(report)
+
+
+def test_one_pass_marginals_26q(genv):
+    """Every qubit's marginal from the one-pass kernel (second query of a
+    state fills the cache) against marginals computed by torch from the
+    state itself, on 26 qubits (2^14 tiles, 11 workgroup bits, 3 varying tile
+    bits)."""
+    import torch
+
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+
+    n = 26
+    r = qa.Register(genv, n)
+    r.init_plus()
+    random_layered(n, 4, seed=26).apply(r)
+    before = qa.capi.getQuESTStats()["marginalPasses"]
+    got = np.array([r.prob(q, 0) for q in range(n)])
+    assert qa.capi.getQuESTStats()["marginalPasses"] - before == 1
+    p = (r.to_torch().abs() ** 2).reshape([2] * n)
+    want = np.array([float(p.sum(dim=tuple(n - 1 - k for k in range(n) if k != q))[0]) for q in range(n)])
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-12)
+    r.close()
