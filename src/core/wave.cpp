@@ -1,6 +1,7 @@
 #include "wave.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
@@ -66,7 +67,119 @@ WaveOp blank(int kind) {
     return w;
 }
 
+// ---- cheaper gate forms (tools/gen_wave_asm.py KINDS2 / PH_KINDS) ----------
+// A rotation [[c, -s], [s, c]] (c^2 + s^2 = 1) runs as three shears with
+// t = tan(phi/2) = s / (1 + c), sn = sin(phi) = s; for c < 0 it is -R(phi - pi):
+// the shears of phi - pi and a factor -1 for the pass (`neg`).
+inline bool unitCircle(double c, double s) { return std::fabs(c * c + s * s - 1) <= 1e-14; }
+
+void rotParams(double c, double s, real* m, bool* neg) {
+    *neg = c < 0;
+    if (*neg) c = -c, s = -s;
+    m[0] = (real)(s / (1 + c));
+    m[1] = (real)s;
+}
+
+inline bool near(double a, double b) { return std::fabs(a - b) <= 1e-15; }
+
+// Kind of a unit-modulus phase p (false: not unit modulus).  DROT / DROTN
+// get their shear parameters in m[0], m[1]; identity phases give kind -1.
+bool phaseKind(double pr, double pi, int* kind, real* m) {
+    if (!unitCircle(pr, pi)) return false;
+    if (near(pr, 1) && near(pi, 0)) *kind = -1;
+    else if (near(pr, -1) && near(pi, 0)) *kind = (int)WKind::DNEG;
+    else if (near(pr, 0) && near(pi, 1)) *kind = (int)WKind::DMULI;
+    else if (near(pr, 0) && near(pi, -1)) *kind = (int)WKind::DMULNI;
+    else {
+        bool neg;
+        rotParams(pr, pi, m, &neg);
+        *kind = neg ? (int)WKind::DROTN : (int)WKind::DROT;
+    }
+    return true;
+}
+
+struct Scale {  // complex factor the pass still owes its amplitudes
+    double re = 1, im = 0;
+    void mul(double r, double i) {
+        const double x = re * r - im * i;
+        im = re * i + im * r;
+        re = x;
+    }
+    bool one() const { return re == 1 && im == 0; }
+};
+
 }  // namespace
+
+// Absorb the factor (sr, si) a pass owes its amplitudes: scale the matrix of
+// one uncontrolled op that takes it at no cost (complex: M2, ANTI, D2S, D2L,
+// LANTI; real: also M2R, M2RI, LM2R, LM2RI); else turn an unnormalised
+// Hadamard or a rotation back into a scaled M2R / M2RI; else append a phase op.
+void settleScale(WaveProgram& out, int begin, double sr, double si) {
+    auto free = [](const WaveOp& w) { return w.cReg == 0 && w.cLane == 0 && w.cLaneZero == 0 && w.ctrlOut == 0; };
+    const bool realF = si == 0;
+    auto cm = [&](real* p) {  // p[0] + i p[1] *= (sr + i si)
+        const double x = p[0] * sr - p[1] * si, y = p[0] * si + p[1] * sr;
+        p[0] = (real)x;
+        p[1] = (real)y;
+    };
+    for (size_t k = (size_t)begin; k < out.ops.size(); k++) {
+        WaveOp& w = out.ops[k];
+        if (!free(w)) continue;
+        switch ((WKind)w.kind) {
+            case WKind::M2:
+                for (int e = 0; e < 4; e++) cm(w.m + 2 * e);
+                return;
+            case WKind::ANTI:
+            case WKind::LANTI:
+            case WKind::D2S:
+            case WKind::D2L:
+                cm(w.m);
+                cm(w.m + 2);
+                return;
+            case WKind::M2R:
+            case WKind::M2RI:
+            case WKind::LM2R:
+            case WKind::LM2RI:
+                if (!realF) break;
+                for (int e = 0; e < 4; e++) w.m[e] = (real)(w.m[e] * sr);
+                return;
+            default: break;
+        }
+    }
+    if (realF)
+        for (size_t k = (size_t)begin; k < out.ops.size(); k++) {
+            WaveOp& w = out.ops[k];
+            if (!free(w)) continue;
+            if (w.kind == (int)WKind::HADD) {  // computed [[1, 1], [1, -1]]
+                w.kind = (int)WKind::M2R;
+                w.m[0] = w.m[1] = w.m[2] = (real)sr;
+                w.m[3] = (real)-sr;
+                return;
+            }
+            if (w.kind == (int)WKind::ROTY || w.kind == (int)WKind::ROTX) {
+                // the emitted rotation: cos = 1 - t sin, sin
+                const double c = 1 - (double)w.m[0] * w.m[1], s = w.m[1];
+                if (w.kind == (int)WKind::ROTY) {
+                    w.m[0] = (real)(c * sr);
+                    w.m[1] = (real)(-s * sr);
+                    w.m[2] = (real)(s * sr);
+                    w.m[3] = (real)(c * sr);
+                    w.kind = (int)WKind::M2R;
+                } else {  // [[c, -is], [-is, c]] as M2RI (m00, Im m01, Im m10, m11)
+                    w.m[0] = (real)(c * sr);
+                    w.m[1] = (real)(-s * sr);
+                    w.m[2] = (real)(-s * sr);
+                    w.m[3] = (real)(c * sr);
+                    w.kind = (int)WKind::M2RI;
+                }
+                return;
+            }
+        }
+    WaveOp w = blank((int)WKind::DIAG);   // every amplitude
+    w.m[0] = (real)sr;
+    w.m[1] = (real)si;
+    out.ops.push_back(w);
+}
 
 int waveTransposeCost(int laneBit) { return laneBit >= kWaveLanes ? 3 : laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
 
@@ -181,9 +294,37 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         lay.put(bl, s);
     };
 
+    // Factors the pass owes its amplitudes (unnormalised Hadamards, rotations
+    // run as -R, global phases split off diagonal gates) are absorbed at the
+    // end by one uncontrolled op whose matrix can take them at no cost (or a
+    // final phase op).  QUEST_WAVE_CHEAP=0 keeps the round-1 kinds only.
+    static const bool cheap = !getenv("QUEST_WAVE_CHEAP") || atoi(getenv("QUEST_WAVE_CHEAP")) != 0;
+    Scale sig;
+    auto uncontrolled = [&](const TileOp& op) { return op.ctrlIn == 0 && op.ctrlOut == 0; };
+    // an uncontrolled general 2x2 absorbs any factor: then every uncontrolled
+    // diagonal gate can drop its global phase; otherwise the first one stays
+    // a D2S / D2L (complex absorber) and the later ones are split
+    bool haveComplexAbsorber = false;
+    for (int i = 0; i < nOps && cheap; i++)
+        if (needsSlot(i) && cls[i] == M2Class::General && uncontrolled(ops[i])) haveComplexAbsorber = true;
+    // phase p on the amplitudes whose tile bits in `mask` are all 1
+    auto emitPhase = [&](unsigned mask, const TileOp& op, double pr, double pi) -> bool {
+        int kind;
+        real pm[2] = {0, 0};
+        if (!cheap || !phaseKind(pr, pi, &kind, pm)) return false;
+        if (kind < 0) return true;   // identity
+        WaveOp w = blank(kind);
+        masks(lay, mask, w.cReg, w.cLane);
+        w.ctrlOut = op.ctrlOut;
+        w.m[0] = pm[0];
+        w.m[1] = pm[1];
+        out.ops.push_back(w);
+        return true;
+    };
     for (int i = 0; i < nOps; i++) {
         const TileOp& op = ops[i];
         if ((OpKind)op.kind == OpKind::Diag) {
+            if (emitPhase(op.ctrlIn, op, op.m[0], op.m[1])) continue;
             WaveOp w = blank((int)WKind::DIAG);
             masks(lay, op.ctrlIn, w.cReg, w.cLane);
             w.ctrlOut = op.ctrlOut;
@@ -197,10 +338,19 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         if (cls[i] == M2Class::Diag) {
             WaveOp w;
             if (m[0] == 1 && m[1] == 0) {  // phase on |1>: diagonal op on ctrl + target
+                if (emitPhase(op.ctrlIn | (1u << t), op, m[6], m[7])) continue;
                 w = blank((int)WKind::DIAG);
                 masks(lay, op.ctrlIn | (1u << t), w.cReg, w.cLane);
                 w.m[0] = m[6];
                 w.m[1] = m[7];
+            } else if (cheap && uncontrolled(op) && haveComplexAbsorber && unitCircle(m[0], m[1]) &&
+                       unitCircle(m[6], m[7])) {
+                // diag(d0, d1) = d0 diag(1, d1 / d0): the pass owes d0
+                sig.mul(m[0], m[1]);
+                const double qr = m[6] * m[0] + m[7] * m[1], qi = m[7] * m[0] - m[6] * m[1];
+                if (emitPhase(1u << t, op, qr, qi)) continue;
+                sig.mul(m[0], -m[1]);  // (not reached: the quotient is unit modulus)
+                w = blank((int)WKind::D2S);
             } else if (!inSlot(lay.where[t]) && laneOf(lay.where[t]) >= kWaveLanes) {
                 // target on a wave bit: d1 on the waves with the bit set, d0
                 // on the others (two wave-uniform phase ops)
@@ -224,6 +374,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 w.m[1] = m[1];
                 w.m[2] = m[6];
                 w.m[3] = m[7];
+                if (uncontrolled(op)) haveComplexAbsorber = true;  // later diagonals may split
             }
             w.ctrlOut = op.ctrlOut;
             out.ops.push_back(w);
@@ -276,9 +427,14 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             transpose(victim, l);
         }
         WaveOp w;
+        bool neg = false;
         switch (cls[i]) {
             case M2Class::Swap: w = blank((int)WKind::SWAP); break;
             case M2Class::Anti:
+                if (cheap && m[2] == 0 && m[4] == 0 && std::fabs(m[3]) == 1 && m[5] == -m[3]) {
+                    w = blank(m[3] < 0 ? (int)WKind::YSW : (int)WKind::YSWC);   // Y = [[0, -i], [i, 0]]
+                    break;
+                }
                 w = blank((int)WKind::ANTI);
                 w.m[0] = m[2];
                 w.m[1] = m[3];
@@ -286,6 +442,22 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 w.m[3] = m[5];
                 break;
             case M2Class::Real:
+                if (cheap && uncontrolled(op) && near(m[0], m[2]) && near(m[0], m[4]) && near(m[0], -m[6])) {
+                    w = blank((int)WKind::HADD);   // m00 [[1, 1], [1, -1]]
+                    sig.mul(m[0], 0);
+                    break;
+                }
+                if (cheap && near(m[0], m[6]) && near(m[2], -m[4]) && unitCircle(m[0], m[4])) {
+                    rotParams(m[0], m[4], w.m, &neg);
+                    if (!neg || uncontrolled(op)) {
+                        const real t0 = w.m[0], t1 = w.m[1];
+                        w = blank((int)WKind::ROTY);
+                        w.m[0] = t0;
+                        w.m[1] = t1;
+                        if (neg) sig.mul(-1, 0);
+                        break;
+                    }
+                }
                 w = blank((int)WKind::M2R);
                 w.m[0] = m[0];
                 w.m[1] = m[2];
@@ -293,6 +465,18 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 w.m[3] = m[6];
                 break;
             case M2Class::RealImag:
+                // [[c, -is], [-is, c]]: m00 = m11 = c, Im m01 = Im m10 = -s
+                if (cheap && near(m[0], m[6]) && near(m[3], m[5]) && unitCircle(m[0], m[5])) {
+                    rotParams(m[0], -m[5], w.m, &neg);
+                    if (!neg || uncontrolled(op)) {
+                        const real t0 = w.m[0], t1 = w.m[1];
+                        w = blank((int)WKind::ROTX);
+                        w.m[0] = t0;
+                        w.m[1] = t1;
+                        if (neg) sig.mul(-1, 0);
+                        break;
+                    }
+                }
                 w = blank((int)WKind::M2RI);
                 w.m[0] = m[0];
                 w.m[1] = m[3];
@@ -309,6 +493,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         w.ctrlOut = op.ctrlOut;
         out.ops.push_back(w);
     }
+    if (!sig.one()) settleScale(out, wp.opBegin, sig.re, sig.im);
     // store layout: tile bits 1-3 back on lane bits 0-2 (bit 0 never left slot 0)
     for (int l = 0; l < 3; l++) {
         const int b = l + 1;

@@ -66,6 +66,18 @@ enum class WKind : int {
     LM2RI = 10,
     LANTI = 11,
     LSWAP = 12,
+    // cheaper forms of common gates on slot a (tools/gen_wave_asm.py KINDS2):
+    ROTY = 13,   // real rotation [[c, -s], [s, c]] by three shears (m = tan(phi/2), sin(phi))
+    ROTX = 14,   // [[c, -is], [-is, c]] (Rx): (a_im, b_re) by +phi, (a_re, b_im) by -phi
+    HADD = 15,   // unnormalised Hadamard (a + b, a - b); never controlled (the pass absorbs 1/sqrt2)
+    YSW = 16,    // Pauli Y as register swaps + sign flips
+    YSWC = 17,   // -Y
+    // unit-modulus phases on the (cReg, cLane) registers (PH_KINDS):
+    DROT = 18,   // multiply by e^{i phi}, |phi| <= pi/2: (re, im) rotated by shears (m as ROTY)
+    DNEG = 19,   // multiply by -1
+    DMULI = 20,  // multiply by i
+    DMULNI = 21, // multiply by -i
+    DROTN = 22,  // multiply by -e^{i phi} (negation + DROT)
 };
 constexpr int kWaveLaneOps = 3;  // lane bits with direct gate handlers
 

@@ -333,7 +333,14 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         return;
     }
     const real* m = w.m;
-    if (kind >= WKind::LM2R) {
+    // the shear rotation of tools/gen_wave_asm.py rot(): same operation order
+    auto rot = [&](real& x, real& y, bool neg) {
+        const real t = neg ? -m[0] : m[0], sn = neg ? -m[1] : m[1];
+        x = std::fma(-t, y, x);
+        y = std::fma(sn, x, y);
+        x = std::fma(-t, y, x);
+    };
+    if (kind >= WKind::LM2R && kind <= WKind::LSWAP) {
         // target on lane bit a: lane pairs (L0, L1 = L0 | 2^a), per register
         const int a = w.a;
         for (int L0 = 0; L0 < kVLanes; L0++) {
@@ -379,6 +386,24 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         if ((unsigned)lane & w.cLaneZero) continue;
         real* r = vr[lane];
         real* i = vi[lane];
+        if (kind >= WKind::DROT && kind <= WKind::DROTN) {
+            for (int j = 0; j < kWaveRegs; j++) {
+                if (((unsigned)j & w.cReg) != w.cReg) continue;
+                real &x = r[j], &y = i[j];
+                if (kind == WKind::DNEG || kind == WKind::DROTN) x = -x, y = -y;
+                if (kind == WKind::DROT || kind == WKind::DROTN) rot(x, y, false);
+                if (kind == WKind::DMULI) {
+                    const real t = x;
+                    x = -y;
+                    y = t;
+                } else if (kind == WKind::DMULNI) {
+                    const real t = x;
+                    x = y;
+                    y = -t;
+                }
+            }
+            continue;
+        }
         if (kind == WKind::DIAG || kind == WKind::D2S || kind == WKind::D2L) {
             for (int j = 0; j < kWaveRegs; j++) {
                 if (((unsigned)j & w.cReg) != w.cReg) continue;
@@ -428,6 +453,32 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
                     r[f] = r0;
                     i[f] = i0;
                     break;
+                case WKind::ROTY:
+                    rot(r[j], r[f], false);
+                    rot(i[j], i[f], false);
+                    break;
+                case WKind::ROTX:
+                    rot(i[j], r[f], false);
+                    rot(r[j], i[f], true);
+                    break;
+                case WKind::HADD:
+                    r[f] = r0 - r1;
+                    r[j] = std::fma((real)2, r0, -r[f]);
+                    i[f] = i0 - i1;
+                    i[j] = std::fma((real)2, i0, -i[f]);
+                    break;
+                case WKind::YSW:  // a -> -i b, b -> i a
+                    r[j] = i1;
+                    i[j] = -r1;
+                    r[f] = -i0;
+                    i[f] = r0;
+                    break;
+                case WKind::YSWC:
+                    r[j] = -i1;
+                    i[j] = r1;
+                    r[f] = i0;
+                    i[f] = -r0;
+                    break;
                 default: break;
             }
         }
@@ -453,7 +504,7 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
         }
     static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;  // planner study: op mix per pass
     if (dump) {
-        int cnt[16] = {0}, trw = 0, ctl = 0;
+        int cnt[32] = {0}, trw = 0, ctl = 0;
         for (int i = ps.opBegin; i < ps.opEnd; i++) {
             const WaveOp& w = wp.ops[(size_t)i];
             cnt[w.kind]++;
@@ -461,9 +512,11 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
             if (w.kind == (int)WKind::TR) g_trCost += waveTransposeCost(w.b);
             if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
         }
-        fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d ctl %d\n",
+        fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d "
+                "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d\n",
                 ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
-                cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl);
+                cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
+                cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22]);
         fprintf(stderr, "wave: cumulative weighted transposition cost %lld\n", g_trCost);
     }
     TilePass tp;

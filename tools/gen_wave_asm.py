@@ -44,7 +44,9 @@ import os as _os
 # WAVE_ST_POLICY override for experiments, e.g. "" or " sc1"
 LD_POLICY = _os.environ.get("WAVE_LD_POLICY", " nt")
 ST_POLICY = _os.environ.get("WAVE_ST_POLICY", " nt")
-OPS_DONE = 256                                 # handler index of the end-of-list sentinel
+# handler index of the end-of-list sentinel (the last table entry; see
+# idx_slot2 / idx_ph for the kinds after 256)
+OPS_DONE = 500
 # handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
 def idx_slot(kind, s, ctrl):
     return KINDS.index(kind) * 16 + s * 2 + ctrl          # 0..79
@@ -76,6 +78,26 @@ def idx_lane(kind, l, ctrl):
 
 def idx_trw(s, b):
     return 200 + s * 4 + b                                 # 200..(200 + 4R), b < 4
+
+
+# cheaper forms of common gates (slot targets): shear rotations (Ry, Rx),
+# the unnormalised Hadamard (its 1/sqrt2 is absorbed by another op of the
+# pass, see src/core/wave.cpp) and Y / -Y as register swaps plus sign flips
+KINDS2 = ["ROTY", "ROTX", "HADD", "YSW", "YSWC"]
+
+
+def idx_slot2(kind, s, ctrl):
+    return 260 + KINDS2.index(kind) * 16 + s * 2 + ctrl    # 260..339
+
+
+# unit-modulus phases on the registers j with (j & creg) == creg (lane = 1:
+# only on lanes whose cLane bits are set): rotation of (re, im) by three
+# shears, negation, multiplication by +-i, negation + rotation
+PH_KINDS = ["DROT", "DNEG", "DMULI", "DMULNI", "DROTN"]
+
+
+def idx_ph(kind, creg, lane):
+    return 340 + PH_KINDS.index(kind) * 32 + creg * 2 + lane  # 340..499 (16 registers)
 
 
 def table_size(R):
@@ -257,9 +279,11 @@ class Gen:
         e("s_addc_u32 s95, s95, 0")
         e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
         e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
+        # flagged ops (bit 31) go to the shared check path: selected as the
+        # jump target rather than branched to (handlers lie > 128 KiB away)
         e("s_bitcmp1_b32 s68, 31")
-        e("s_cbranch_scc1 .Lcheck")
-        e("s_add_u32 s98, s92, s68")                   # kernel base + handler offset
+        e("s_cselect_b32 s98, .Lcheck-qa_wave_tile, s68")
+        e("s_add_u32 s98, s92, s98")                   # kernel base + handler offset
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
 
@@ -362,8 +386,38 @@ class Gen:
             for a, b in ((self.re(j), self.re(f)), (self.im(j), self.im(f))):
                 e(f"v_swap_b32 v{a}, v{b}")
                 e(f"v_swap_b32 v{a + 1}, v{b + 1}")
+        elif kind == "ROTY":   # (a, b) -> (c a - s b, s a + c b) on re and im: m = tan(phi/2), sin(phi)
+            for base in (self.re, self.im):
+                self.rot(base(j), base(f), False)
+        elif kind == "ROTX":   # a -> c a - i s b, b -> -i s a + c b: (a_im, b_re) by +phi, (a_re, b_im) by -phi
+            self.rot(self.im(j), self.re(f), False)
+            self.rot(self.re(j), self.im(f), True)
+        elif kind == "HADD":   # (a, b) -> (a + b, a - b), unnormalised
+            for base in (self.re, self.im):
+                a, b = self.vp(base(j)), self.vp(base(f))
+                e(f"v_add_f64 {b}, {a}, -{b}")
+                e(f"v_fma_f64 {a}, 2.0, {a}, -{b}")
+        elif kind in ("YSW", "YSWC"):
+            # Y: a -> -i b, b -> i a  (YSWC: -Y): swap a_re <-> b_im, a_im <-> b_re, then two sign flips
+            for x, y in ((self.re(j), self.im(f)), (self.im(j), self.re(f))):
+                e(f"v_swap_b32 v{x}, v{y}")
+                e(f"v_swap_b32 v{x + 1}, v{y + 1}")
+            neg = (self.im(j), self.re(f)) if kind == "YSW" else (self.re(j), self.im(f))
+            for r in neg:
+                e(f"v_xor_b32_e32 v{r + 1}, 0x80000000, v{r + 1}")
         else:
             raise ValueError(kind)
+
+    def rot(self, x, y, neg):
+        """Rotate the register pair (x, y) by phi (neg: by -phi) in place with
+        three shears: x -= t y; y += s x; x -= t y  (t = tan(phi/2) in m[0],
+        s = sin(phi) in m[1]): 3 FMAs per pair instead of 4 multiplies + adds."""
+        t, sn = self.sm(0), self.sm(1)
+        mt, ps = (t, "-" + sn) if neg else ("-" + t, sn)
+        X, Y = self.vp(x), self.vp(y)
+        self.e(f"v_fma_f64 {X}, {mt}, {Y}, {X}")
+        self.e(f"v_fma_f64 {Y}, {ps}, {X}, {Y}")
+        self.e(f"v_fma_f64 {X}, {mt}, {Y}, {X}")
 
     def cmul_sgpr(self, j, kr, ki, ts=0):
         # (x + iy) *= (m[kr] + i m[ki])
@@ -402,6 +456,55 @@ class Gen:
             self.ctrl_end()
         else:
             self.end_region()
+        self.back()
+
+    def gen_slot2(self, kind, s, ctrl):
+        self.handler(idx_slot2(kind, s, ctrl), f"{kind}_s{s}_c{ctrl}")
+        if ctrl:
+            self.ctrl_begin()
+        else:
+            self.region()
+        for p, j in enumerate([j for j in range(self.NS) if not (j >> s) & 1]):
+            f = j | (1 << s)
+            if ctrl:
+                skip = f".Lskip_{kind}_{s}_{j}"
+                self.ctrl_j(j, skip)
+                self.pair(kind, j, f)
+                self.label(skip)
+            else:
+                self.pair(kind, j, f)
+        if ctrl:
+            self.ctrl_end()
+        else:
+            self.end_region()
+        self.back()
+
+    def gen_ph(self, kind, creg, lane):
+        """Unit-modulus phase on the registers j with (j & creg) == creg of
+        the lanes whose cLane (s70) bits are set (lane = 1; exec-masked)."""
+        self.handler(idx_ph(kind, creg, lane), f"{kind}_m{creg}_l{lane}")
+        e = self.e
+        if lane:
+            e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
+            e(f"v_cmp_eq_u32_e64 s[96:97], s70, v{self.vTmp}")
+            e("s_nop 4")
+            e("s_mov_b64 exec, s[96:97]")
+        self.region()
+        for j in [j for j in range(self.NS) if (j & creg) == creg]:
+            x, y = self.re(j), self.im(j)
+            if kind in ("DNEG", "DROTN"):
+                e(f"v_xor_b32_e32 v{x + 1}, 0x80000000, v{x + 1}")
+                e(f"v_xor_b32_e32 v{y + 1}, 0x80000000, v{y + 1}")
+            if kind in ("DROT", "DROTN"):
+                self.rot(x, y, False)
+            elif kind in ("DMULI", "DMULNI"):   # x + iy -> -y + ix  /  y - ix
+                e(f"v_swap_b32 v{x}, v{y}")
+                e(f"v_swap_b32 v{x + 1}, v{y + 1}")
+                r = x if kind == "DMULI" else y
+                e(f"v_xor_b32_e32 v{r + 1}, 0x80000000, v{r + 1}")
+        self.end_region()
+        if lane:
+            e("s_mov_b64 exec, -1")
         self.back()
 
     def gen_d2s(self, s, ctrl):
@@ -866,6 +969,17 @@ class Gen:
             for l in range(LANE_BITS):
                 for c in (0, 1):
                     self.gen_lane(kind, l, c)
+        for kind in KINDS2:
+            for s in range(R):
+                for c in (0, 1):
+                    if kind == "HADD" and c:
+                        continue   # only uncontrolled Hadamards drop their 1/sqrt2
+                    self.gen_slot2(kind, s, c)
+        assert NS <= 16, "idx_ph reserves 32 entries per phase kind"
+        for kind in PH_KINDS:
+            for creg in range(NS):
+                for lane in (0, 1):
+                    self.gen_ph(kind, creg, lane)
         L.append(".Lfunc_end0:")
         L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
         self.descriptor()
@@ -1071,6 +1185,7 @@ def main():
         f.write(f"static const int kWaveImageWBits = {args.wbits};\n")
         vg = re.search(r"amdhsa_next_free_vgpr (\d+)", open(args.out.replace("wave_image.inc", "wave_kernel.s")).read())
         f.write(f"static const int kWaveImageVgprs = {vg.group(1)};\n")
+        f.write(f"static const int kWaveSentinelIndex = {OPS_DONE};\n")
         f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
         f.write(f"static const unsigned char kWaveImage[{len(img)}] __attribute__((aligned(4096))) = {{\n")
         for k in range(0, len(img), 24):

@@ -25,7 +25,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-GATE_KERNELS = ("qa_wave_tile", "tilePass", "Tile", "Direct")
+GATE_KERNELS = ("qa_wave_tile", "tilePassKernel", "DirectKernel", "mat2LowKernel")
 
 
 def run(args):

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--qubits", type=int, default=28)
     ap.add_argument("--count", type=int, default=32)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="", help="regex: run only the matching workloads (plus the base pass)")
     args = ap.parse_args()
     import quest_amd as qa
     from quest_amd.ops import capi
@@ -62,6 +63,10 @@ def main():
         "mid M2R x96": lambda: [(reg.h(0), reg.h(4), reg.cz(0, 4)) for i in range(48)],
         "mid DIAG x96": lambda: [reg.t(i % 4) for i in range(96)],
     }
+    if args.only:
+        import re
+
+        workloads = {k: v for k, v in workloads.items() if k.startswith("base") or re.search(args.only, k)}
     res = {}
     for r in range(args.reps):
         for name, fn in workloads.items():
