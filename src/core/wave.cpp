@@ -183,25 +183,48 @@ void settleScale(WaveProgram& out, int begin, double sr, double si) {
 
 int waveTransposeCost(int laneBit) { return laneBit >= kWaveLanes ? 3 : laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
 
+bool waveChannel(const real* m) {
+    for (int e = 0; e < 16; e++) {
+        if (m[2 * e + 1] != 0) return false;
+        const int r = e >> 2, c = e & 3;
+        const bool allowed = (r == c) || (r == 0 && c == 3) || (r == 3 && c == 0);
+        if (!allowed && m[2 * e] != 0) return false;
+    }
+    return m[2 * 5] == m[2 * 10];
+}
+
 bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out) {
     if (ps.k != kWaveBits) return false;
     for (int i = 0; i < 4; i++)
         if (ps.pos[i] != i) return false;
     std::vector<M2Class> cls(nOps, M2Class::Diag);
+    std::vector<char> chan(nOps, 0);   // one-qubit density channel (CH1 / CHD) on t[0], t[1]
     for (int i = 0; i < nOps; i++) {
         const OpKind k = (OpKind)ops[i].kind;
         if (k == OpKind::Mat2)
             cls[i] = classify(ops[i].m);
+        else if (k == OpKind::Mat4 && waveChannel(ops[i].m) && ops[i].ctrlIn == 0 && ops[i].ctrlOut == 0)
+            chan[i] = 1;
         else if (k != OpKind::Diag)
             return false;
     }
-    // ops that need their target in a register slot
+    // ops that need their target(s) in a register slot
     auto needsSlot = [&](int i) { return (OpKind)ops[i].kind == OpKind::Mat2 && cls[i] != M2Class::Diag; };
+    auto slotTargets = [&](int i, int* t) {
+        if (chan[i]) {
+            t[0] = ops[i].t[0];
+            t[1] = ops[i].t[1];
+            return 2;
+        }
+        t[0] = ops[i].t[0];
+        return needsSlot(i) ? 1 : 0;
+    };
     // next[i][b]: first op >= i needing tile bit b in a slot
     std::vector<int> nextNeed((size_t)(nOps + 1) * kWaveBits, kInf);
     for (int i = nOps - 1; i >= 0; i--) {
         for (int b = 0; b < kWaveBits; b++) nextNeed[(size_t)i * kWaveBits + b] = nextNeed[(size_t)(i + 1) * kWaveBits + b];
-        if (needsSlot(i)) nextNeed[(size_t)i * kWaveBits + ops[i].t[0]] = i;
+        int t[2];
+        for (int k = 0, n = slotTargets(i, t); k < n; k++) nextNeed[(size_t)i * kWaveBits + t[k]] = i;
     }
     auto nextUse = [&](int i, int b) { return nextNeed[(size_t)i * kWaveBits + b]; };
     // remaining[i][b]: ops >= i needing tile bit b in a slot
@@ -209,7 +232,8 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     for (int i = nOps - 1; i >= 0; i--) {
         for (int b = 0; b < kWaveBits; b++)
             remaining[(size_t)i * kWaveBits + b] = remaining[(size_t)(i + 1) * kWaveBits + b];
-        if (needsSlot(i)) remaining[(size_t)i * kWaveBits + ops[i].t[0]]++;
+        int t[2];
+        for (int k = 0, n = slotTargets(i, t); k < n; k++) remaining[(size_t)i * kWaveBits + t[k]]++;
     }
     // a gate on lane bit 0-2 runs there directly (DPP partner fetch: about one
     // transposition of work, twice a slot gate) unless the bit has enough slot
@@ -321,8 +345,41 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         out.ops.push_back(w);
         return true;
     };
+    // bring tile bit b into a register slot (not the slot `keep`), evicting
+    // the slot whose next use lies furthest (slot 0 keeps tile bit 0)
+    auto toSlot = [&](int i, int b, int keep) {
+        if (inSlot(lay.where[b])) return;
+        const int l = laneOf(lay.where[b]);
+        int victim = -1, far = -1;
+        for (int s = 1; s < kWaveSlots; s++) {
+            if (s == keep) continue;
+            const int nu = nextUse(i, lay.slotBit[s]);
+            if (nu > far) {
+                far = nu;
+                victim = s;
+            }
+        }
+        transpose(victim, l);
+    };
     for (int i = 0; i < nOps; i++) {
         const TileOp& op = ops[i];
+        if (chan[i]) {
+            const int r = op.t[0], c = op.t[1];
+            toSlot(i, r, inSlot(lay.where[c]) ? lay.where[c] : -1);
+            toSlot(i, c, lay.where[r]);
+            const real* m = op.m;
+            const bool dephaseOnly = m[0] == 1 && m[2 * 3] == 0 && m[2 * 12] == 0 && m[2 * 15] == 1;
+            WaveOp w = blank(dephaseOnly ? (int)WKind::CHD : (int)WKind::CH1);
+            w.a = lay.where[r];
+            w.b = lay.where[c];
+            w.m[0] = m[0];
+            w.m[1] = m[2 * 3];
+            w.m[2] = m[2 * 12];
+            w.m[3] = m[2 * 15];
+            w.m[4] = m[2 * 5];
+            out.ops.push_back(w);
+            continue;
+        }
         if ((OpKind)op.kind == OpKind::Diag) {
             if (emitPhase(op.ctrlIn, op, op.m[0], op.m[1])) continue;
             WaveOp w = blank((int)WKind::DIAG);

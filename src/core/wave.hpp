@@ -78,7 +78,17 @@ enum class WKind : int {
     DMULI = 20,  // multiply by i
     DMULNI = 21, // multiply by -i
     DROTN = 22,  // multiply by -e^{i phi} (negation + DROT)
+    // one-qubit density channels on the 4-group of slots (a = row bit, b =
+    // column bit; g = bit a + 2 bit b): x0, x3 mixed by the real 2x2 m[0..3],
+    // x1, x2 scaled by m[4] (CHD: the scaling only)
+    CH1 = 23,
+    CHD = 24,
 };
+
+// Whether a Mat4 (4x4, row-major, interleaved re/im as in TileOp::m) is a
+// one-qubit channel superoperator the wave engine runs (CH1 / CHD): real,
+// nonzero only at (0,0) (0,3) (3,0) (3,3) and (1,1) = (2,2).
+bool waveChannel(const real* m);
 constexpr int kWaveLaneOps = 3;  // lane bits with direct gate handlers
 
 // One op, uploaded as-is (uniform: read through the scalar cache).

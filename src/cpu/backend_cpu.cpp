@@ -386,6 +386,23 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         if ((unsigned)lane & w.cLaneZero) continue;
         real* r = vr[lane];
         real* i = vi[lane];
+        if (kind == WKind::CH1 || kind == WKind::CHD) {
+            const int a = w.a, b = w.b;
+            for (int j = 0; j < kWaveRegs; j++) {
+                if (((j >> a) & 1) || ((j >> b) & 1)) continue;
+                const int x1 = j | (1 << a), x2 = j | (1 << b), x3 = x1 | (1 << b);
+                for (real* v : {r, i}) {
+                    v[x1] *= m[4];
+                    v[x2] *= m[4];
+                    if (kind == WKind::CH1) {
+                        const real t = m[2] * v[j];
+                        v[j] = std::fma(m[1], v[x3], m[0] * v[j]);
+                        v[x3] = std::fma(m[3], v[x3], t);
+                    }
+                }
+            }
+            continue;
+        }
         if (kind >= WKind::DROT && kind <= WKind::DROTN) {
             for (int j = 0; j < kWaveRegs; j++) {
                 if (((unsigned)j & w.cReg) != w.cReg) continue;
@@ -513,10 +530,10 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
             if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
         }
         fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d "
-                "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d\n",
+                "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d chan %d\n",
                 ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
                 cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
-                cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22]);
+                cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24]);
         fprintf(stderr, "wave: cumulative weighted transposition cost %lld\n", g_trCost);
     }
     TilePass tp;

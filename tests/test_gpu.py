@@ -106,6 +106,40 @@ def test_density_gates_and_noise(genv, n):
     reg.close()
 
 
+@pytest.mark.parametrize("n", [10])
+def test_density_one_qubit_channels_on_wave_engine(genv, n):
+    """A density matrix of 10 qubits (2^20 amplitudes, the smallest the wave
+    engine takes; the dense NumPy oracle is too slow beyond) under
+    gates and one-qubit dephasing, depolarising and damping: every pass runs
+    on the wave engine (channels as CH1 / CHD register ops on the row and
+    column bits), against the NumPy oracle."""
+    import quest_amd as qa
+    from helpers import apply_random_ops, assert_close, oracle_for
+    from quest_amd.utils import oracle as O
+
+    rng = np.random.default_rng(300 + n)
+    reg = qa.Register(genv, n, density=True)
+    o = oracle_for(reg, rng)
+    qa.capi.resetQuESTStats()
+    apply_random_ops(reg, o, rng, 30)
+    for k in range(40):
+        a = int(rng.integers(n))
+        p = float(rng.uniform(0, 0.5))
+        [(reg.dephase, o.dephase), (reg.depolarise, o.depolarise), (reg.damping, o.damping)][k % 3][0](a, p)
+        [(reg.dephase, o.dephase), (reg.depolarise, o.depolarise), (reg.damping, o.damping)][k % 3][1](a, p)
+        if k % 5 == 0:
+            reg.h(a)
+            o.apply(O.H, a)
+    reg.sync()
+    st = qa.capi.getQuESTStats()
+    assert st["wavePasses"] > 0 and st["wavePasses"] == st["passes"], st
+    assert_close(reg, o, tol=1e-9)
+    assert abs(reg.purity() - o.purity()) < 1e-10
+    for q in range(n):
+        assert abs(reg.prob(q, 0) - o.prob(q, 0)) < 1e-10
+    reg.close()
+
+
 @pytest.mark.parametrize("fusion", [True, False])
 @pytest.mark.parametrize("n", [14, 20])
 def test_random_circuit_fused_and_eager(genv, n, fusion):

@@ -45,8 +45,8 @@ import os as _os
 LD_POLICY = _os.environ.get("WAVE_LD_POLICY", " nt")
 ST_POLICY = _os.environ.get("WAVE_ST_POLICY", " nt")
 # handler index of the end-of-list sentinel (the last table entry; see
-# idx_slot2 / idx_ph for the kinds after 256)
-OPS_DONE = 500
+# idx_slot2 / idx_ph / idx_ch for the kinds after 256)
+OPS_DONE = 532
 # handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
 def idx_slot(kind, s, ctrl):
     return KINDS.index(kind) * 16 + s * 2 + ctrl          # 0..79
@@ -98,6 +98,17 @@ PH_KINDS = ["DROT", "DNEG", "DMULI", "DMULNI", "DROTN"]
 
 def idx_ph(kind, creg, lane):
     return 340 + PH_KINDS.index(kind) * 32 + creg * 2 + lane  # 340..499 (16 registers)
+
+
+# one-qubit density-matrix channels: a real superoperator on the 4-group of
+# slots (a, b) = (row bit, column bit), g = bit a + 2 bit b: CH1 mixes
+# (x0, x3) by a real 2x2 (m0 m1 / m2 m3) and scales x1, x2 by m4 (dephasing,
+# depolarising, amplitude damping, density collapse); CHD only scales x1, x2
+CH_KINDS = ["CH1", "CHD"]
+
+
+def idx_ch(kind, a, b):
+    return 500 + CH_KINDS.index(kind) * 16 + a * 4 + b     # 500..531 (4 slots)
 
 
 def table_size(R):
@@ -505,6 +516,29 @@ class Gen:
         self.end_region()
         if lane:
             e("s_mov_b64 exec, -1")
+        self.back()
+
+    def gen_ch(self, kind, a, b):
+        self.handler(idx_ch(kind, a, b), f"{kind}_a{a}_b{b}")
+        e = self.e
+        self.region()
+        k = 0
+        for j in range(self.NS):
+            if (j >> a) & 1 or (j >> b) & 1:
+                continue
+            x = [j, j | (1 << a), j | (1 << b), j | (1 << a) | (1 << b)]
+            for base in (self.re, self.im):
+                X = [self.vp(base(r)) for r in x]
+                e(f"v_mul_f64 {X[1]}, {self.sm(4)}, {X[1]}")
+                e(f"v_mul_f64 {X[2]}, {self.sm(4)}, {X[2]}")
+                if kind == "CH1":
+                    T = self.vp(self.T[k % 16])
+                    k += 1
+                    e(f"v_mul_f64 {T}, {self.sm(2)}, {X[0]}")
+                    e(f"v_mul_f64 {X[0]}, {self.sm(0)}, {X[0]}")
+                    e(f"v_fma_f64 {X[0]}, {self.sm(1)}, {X[3]}, {X[0]}")
+                    e(f"v_fma_f64 {X[3]}, {self.sm(3)}, {X[3]}, {T}")
+        self.end_region()
         self.back()
 
     def gen_d2s(self, s, ctrl):
@@ -975,7 +1009,12 @@ class Gen:
                     if kind == "HADD" and c:
                         continue   # only uncontrolled Hadamards drop their 1/sqrt2
                     self.gen_slot2(kind, s, c)
-        assert NS <= 16, "idx_ph reserves 32 entries per phase kind"
+        assert NS <= 16 and R <= 4, "idx_ph reserves 32 entries per phase kind, idx_ch 16 per channel kind"
+        for kind in CH_KINDS:
+            for a in range(R):
+                for b in range(R):
+                    if a != b:
+                        self.gen_ch(kind, a, b)
         for kind in PH_KINDS:
             for creg in range(NS):
                 for lane in (0, 1):
