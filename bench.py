@@ -142,7 +142,7 @@ def main():
         "higher_is_better": False,
         "scaling": "weak",
         "vs_baseline": s_per_gate / BASELINE_S_PER_OP,
-        "dtype": "fp64",
+        "dtype": "fp64" if qa.capi.binding().prec == 2 else "fp32",
         "data": "synthetic: |+>^n initial state, seeded random layered circuit",
         "config": {
             "model": f"random layered circuit (1q gate on every qubit + CNOT brick), {n} qubits",

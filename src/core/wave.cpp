@@ -71,7 +71,11 @@ WaveOp blank(int kind) {
 // A rotation [[c, -s], [s, c]] (c^2 + s^2 = 1) runs as three shears with
 // t = tan(phi/2) = s / (1 + c), sn = sin(phi) = s; for c < 0 it is -R(phi - pi):
 // the shears of phi - pi and a factor -1 for the pass (`neg`).
-inline bool unitCircle(double c, double s) { return std::fabs(c * c + s * s - 1) <= 1e-14; }
+// tolerances for recognising unit-modulus / structured matrices: a few ulps
+// of the build's precision (the matrices arrive in qreal)
+constexpr double kUnitTol = sizeof(real) == 8 ? 1e-14 : 1e-6;
+constexpr double kNearTol = sizeof(real) == 8 ? 1e-15 : 1e-7;
+inline bool unitCircle(double c, double s) { return std::fabs(c * c + s * s - 1) <= kUnitTol; }
 
 void rotParams(double c, double s, real* m, bool* neg) {
     *neg = c < 0;
@@ -80,7 +84,7 @@ void rotParams(double c, double s, real* m, bool* neg) {
     m[1] = (real)s;
 }
 
-inline bool near(double a, double b) { return std::fabs(a - b) <= 1e-15; }
+inline bool near(double a, double b) { return std::fabs(a - b) <= kNearTol; }
 
 // Kind of a unit-modulus phase p (false: not unit modulus).  DROT / DROTN
 // get their shear parameters in m[0], m[1]; identity phases give kind -1.
@@ -195,7 +199,7 @@ bool waveChannel(const real* m) {
 
 bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out) {
     if (ps.k != kWaveBits) return false;
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < kWaveVecBits + 3; i++)
         if (ps.pos[i] != i) return false;
     std::vector<M2Class> cls(nOps, M2Class::Diag);
     std::vector<char> chan(nOps, 0);   // one-qubit density channel (CH1 / CHD) on t[0], t[1]
@@ -244,25 +248,27 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
 
     WavePass wp;
     for (int i = 0; i < kWaveBits; i++) wp.pos[i] = ps.pos[i];
-    // load layout: bit 0 -> slot 0, bits 1-3 -> lanes 0-2; of the higher tile
-    // bits those needed in a slot earliest take the other slots, the rest
-    // lanes 3-5
+    // load layout: the vector bits (fp64: tile bit 0, fp32: bits 0-1) in
+    // slots 0.., the next three on lanes 0-2 (8 lanes x 16 bytes = one 128-byte
+    // line); of the higher tile bits those needed in a slot earliest take the
+    // other slots, the rest lanes 3-5 and the wave bits
+    constexpr int VB = kWaveVecBits;
     Layout lay;
-    lay.put(0, 0);
-    for (int l = 0; l < 3; l++) lay.put(l + 1, kWaveSlots + l);
+    for (int v = 0; v < VB; v++) lay.put(v, v);
+    for (int l = 0; l < 3; l++) lay.put(VB + l, kWaveSlots + l);
     std::vector<int> high;
-    for (int b = 4; b < kWaveBits; b++) high.push_back(b);
+    for (int b = VB + 3; b < kWaveBits; b++) high.push_back(b);
     // bits above kWaveLanePosMax may not sit on real lanes (32-bit per-lane
     // offsets); wave bits take any position (per-wave uniform offsets)
     auto farPos = [&](int b) { return ps.pos[b] > kWaveLanePosMax; };
     int nFar = 0;
     for (int b : high) nFar += farPos(b);
-    if (nFar > (kWaveSlots - 1) + kWaveWBits) return false;
+    if (nFar > (kWaveSlots - VB) + kWaveWBits) return false;
     // slots: the bits needed in a slot earliest; then real lanes 3-5 for the
     // next near bits, wave bits for the rest (LDS transpositions are dearest)
     std::stable_sort(high.begin(), high.end(), [&](int x, int y) { return nextUse(0, x) < nextUse(0, y); });
-    std::vector<int> slots(high.begin(), high.begin() + (kWaveSlots - 1));
-    std::vector<int> rest(high.begin() + (kWaveSlots - 1), high.end());
+    std::vector<int> slots(high.begin(), high.begin() + (kWaveSlots - VB));
+    std::vector<int> rest(high.begin() + (kWaveSlots - VB), high.end());
     // real lanes 3-5: three near bits, from the rest first (in need order);
     // if the rest has fewer, near bits leave the slots for them and far bits
     // of the rest take their slot places
@@ -301,7 +307,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         waves.erase(waves.begin() + far);
     }
     if ((int)lanes.size() != kWaveLanes - 3 || (int)waves.size() != kWaveWBits) return false;
-    for (int s = 1; s < kWaveSlots; s++) lay.put(slots[s - 1], s);
+    for (int s = VB; s < kWaveSlots; s++) lay.put(slots[s - VB], s);
     for (int l = 3; l < kWaveLanes; l++) lay.put(lanes[l - 3], kWaveSlots + l);
     for (int l = kWaveLanes; l < kWaveLaneBits; l++) lay.put(waves[l - kWaveLanes], kWaveSlots + l);
     for (int s = 0; s < kWaveSlots; s++) wp.ldSlot[s] = lay.slotBit[s];
@@ -351,7 +357,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         if (inSlot(lay.where[b])) return;
         const int l = laneOf(lay.where[b]);
         int victim = -1, far = -1;
-        for (int s = 1; s < kWaveSlots; s++) {
+        for (int s = VB; s < kWaveSlots; s++) {
             if (s == keep) continue;
             const int nu = nextUse(i, lay.slotBit[s]);
             if (nu > far) {
@@ -474,7 +480,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         if (!inSlot(lay.where[t])) {
             const int l = laneOf(lay.where[t]);
             int victim = 1, far = -1;
-            for (int s = 1; s < kWaveSlots; s++) {
+            for (int s = VB; s < kWaveSlots; s++) {
                 const int nu = nextUse(i, lay.slotBit[s]);
                 if (nu > far) {
                     far = nu;
@@ -551,24 +557,25 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         out.ops.push_back(w);
     }
     if (!sig.one()) settleScale(out, wp.opBegin, sig.re, sig.im);
-    // store layout: tile bits 1-3 back on lane bits 0-2 (bit 0 never left slot 0)
+    // store layout: tile bits VB..VB+2 back on lane bits 0-2 (the vector bits
+    // never left their slots)
     for (int l = 0; l < 3; l++) {
-        const int b = l + 1;
+        const int b = VB + l;
         const int w = lay.where[b];
         if (w == kWaveSlots + l) continue;
         if (inSlot(w)) {
             transpose(w, l);
         } else {
-            // b sits on another lane bit (>= 3): through slot 1
-            transpose(1, laneOf(w));
-            transpose(1, l);
+            // b sits on another lane bit (>= 3): through the first free slot
+            transpose(VB, laneOf(w));
+            transpose(VB, l);
         }
     }
     // real lane bits 3.. may not carry positions above kWaveLanePosMax at store
     for (int l = 3; l < kWaveLanes; l++) {
         if (!farPos(lay.laneBit[l])) continue;
         int s = -1;
-        for (int x = 1; x < kWaveSlots && s < 0; x++)
+        for (int x = VB; x < kWaveSlots && s < 0; x++)
             if (!farPos(lay.slotBit[x])) s = x;
         if (s < 0) return false;  // cannot happen: at most kWaveSlots - 1 far bits
         transpose(s, l);

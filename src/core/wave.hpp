@@ -1,5 +1,5 @@
 // Wave-tile programs: the register-resident pass engine of the HIP backend
-// (fp64), planned on the host.
+// (fp64 and fp32), planned on the host.
 //
 // A pass of the ordinary tile planner (tiles.hpp) with exactly kWaveBits tile
 // bits is executed by ONE wave per tile: each of the 64 lanes holds 16
@@ -32,12 +32,22 @@
 
 namespace qa {
 
-#ifndef QA_WAVE_SLOTS
-#define QA_WAVE_SLOTS 4
+// Register slots: 2^4 fp64 / 2^5 fp32 amplitudes per lane (the same 64
+// VGPRs of tile); QA_WAVE_SLOTS_F64 / _F32 override (make WAVE_SLOTS=...)
+#ifndef QA_WAVE_SLOTS_F64
+#define QA_WAVE_SLOTS_F64 4
 #endif
-// 2^4 amplitudes per lane: with 2^5 the compiler could not keep the
-// loop-carried tile in registers (spills at any occupancy)
-constexpr int kWaveSlots = QA_WAVE_SLOTS;
+#ifndef QA_WAVE_SLOTS_F32
+#define QA_WAVE_SLOTS_F32 5
+#endif
+#if QuEST_PREC == 1
+constexpr int kWaveSlots = QA_WAVE_SLOTS_F32;
+#else
+constexpr int kWaveSlots = QA_WAVE_SLOTS_F64;
+#endif
+// tile bits inside one 16-byte vector (they stay in slots 0.. for the whole
+// pass): fp64 tile bit 0, fp32 tile bits 0-1
+constexpr int kWaveVecBits = sizeof(real) == 8 ? 1 : 2;
 constexpr int kWaveLanes = 6;   // 64 lanes
 // A tile is shared by 2^kWaveWBits waves of a workgroup: "wave bits" are
 // virtual lane bits 6.. of the tile (transpositions with a slot go through
@@ -48,7 +58,8 @@ constexpr int kWaveLanes = 6;   // 64 lanes
 constexpr int kWaveWBits = QA_WAVE_WBITS;
 constexpr int kWaveLaneBits = kWaveLanes + kWaveWBits;  // real + wave lane bits
 constexpr int kWaveBits = kWaveSlots + kWaveLaneBits;
-constexpr int kWaveLanePosMax = 27;
+// real lane bits carry positions up to this (32-bit per-lane byte offsets)
+constexpr int kWaveLanePosMax = sizeof(real) == 8 ? 27 : 28;
 
 enum class WKind : int {
     M2 = 0,    // general 2x2 on slot a

@@ -56,6 +56,39 @@ def test_wave_kernel_every_gate_kind_gpu():
 
 
 @pytest.mark.gpu
+def test_fp32_wave_kernel_every_gate_kind_gpu():
+    """The fp32 wave kernel (--prec 1: one VGPR per value, 32 amplitudes per
+    lane, tile bits 0-1 in the 16-byte vector) per gate kind against the
+    oracle, in a subprocess bound to the fp32 HIP library."""
+    out = _run([os.path.join(ROOT, "tools", "wave_kinds.py"), "--qubits", "22", "--count", "40"],
+               {"QUEST_PREC": "1", "QUEST_BACKEND": "hip"}, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
+    assert "bad: []" in out.stdout and " wave 0 " not in out.stdout
+
+
+@pytest.mark.gpu
+def test_fp32_wave_matches_fp64_layered_24q_gpu():
+    """A 24-qubit random layered circuit on the fp32 wave engine agrees with
+    the fp64 library to fp32 precision (and ran on wave passes)."""
+    code = ("import numpy as np, quest_amd as qa\n"
+            "from quest_amd.models import random_layered\n"
+            "e = qa.Env(); r = qa.Register(e, 24); r.init_plus(); qa.capi.resetQuESTStats()\n"
+            "random_layered(24, 12, seed=5).apply(r); r.sync()\n"
+            "st = qa.capi.getQuESTStats(); assert st['wavePasses'] > 0, st\n"
+            "np.save('{out}', r.to_numpy().astype(np.complex128))\n")
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        res = {}
+        for prec in ("1", "2"):
+            f = os.path.join(d, f"s{prec}.npy")
+            out = _run(["-c", code.format(out=f)], {"QUEST_PREC": prec, "QUEST_BACKEND": "hip"}, timeout=300)
+            assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+            res[prec] = np.load(f)
+        err = np.max(np.abs(res["1"] - res["2"]))
+        assert err < 1e-5 * 2 ** -12 * 40, err   # amplitudes ~2^-12, fp32 per-gate rounding
+
+
+@pytest.mark.gpu
 def test_wave_kernel_matches_lds_kernel_gpu(env):
     import quest_amd as qa
     from quest_amd.models import random_layered

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generator of the wave-tile pass kernel in gfx950 assembly (fp64).
+"""Generator of the wave-tile pass kernel in gfx950 assembly (fp64 or fp32).
 
 Why assembly: the kernel keeps a 2^(R+6)-amplitude tile in VGPRs across a
 runtime-dispatched list of ops.  Written in HIP C++, LLVM's structurizer and
@@ -10,14 +10,20 @@ place; the host plan (src/core/wave.hpp) picks the handler of each op, whose
 byte offset from the dispatch anchor is stored in the op record, and the
 kernel jumps there with s_setpc_b64.
 
-    python tools/gen_wave_asm.py asm   --slots 4 --out build/wave/wave_kernel.s
-    python tools/gen_wave_asm.py embed --obj build/wave/wave_kernel.o \
-        --hsaco build/wave/wave_kernel.hsaco --out build/wave/wave_image.inc
+    python tools/gen_wave_asm.py asm   --prec 2 --slots 4 --out build/wave_f64/wave_kernel.s
+    python tools/gen_wave_asm.py embed --prec 2 --obj build/wave_f64/wave_kernel.o \
+        --hsaco build/wave_f64/wave_kernel.hsaco --out build/wave_f64/wave_image.inc
 
-Register plan (R = slots, NS = 2^R amplitudes per lane):
-    v[2j : 2j+1]              re of register j        (j < NS)
-    v[2NS+2j : 2NS+2j+1]      im of register j
-    T0..T3 (4 doubles)        temporaries;  C0, C1 per-lane coefficients
+fp64 (--prec 2): a value is a VGPR pair, 2 values per 16-byte vector (tile
+bit 0 in slot 0).  fp32 (--prec 1, the reference's QuEST_PREC=1 build,
+QuEST_precision.h:17-62): one VGPR per value, 4 per vector (tile bits 0-1 in
+slots 0-1) and 32 amplitudes per lane (--slots 5): the same registers and
+bytes per tile, twice the amplitudes, full-rate fp32 arithmetic.
+
+Register plan (R = slots, NS = 2^R amplitudes per lane, P = dwords per value):
+    v[Pj : Pj+P-1]            re of register j        (j < NS)
+    v[P NS + Pj ...]          im of register j
+    T0..T15 (16 values)       temporaries;  C0, C1 per-lane coefficients
     vLane / vLdB / vStB       lane id, per-lane load / store byte offsets
 Device records (host side: src/hip/backend_hip.hip, WaveLaunchDev / WaveOpDev):
     launch + 0    u64 numTiles          + 8   u64 waveStride
@@ -28,7 +34,7 @@ Device records (host side: src/hip/backend_hip.hip, WaveLaunchDev / WaveOpDev):
            + 1280 u64 debugBuf
            pos[b] for b >= 12 sits in bits 8.. of pos[b - 12]
            + 2048 WaveOpDev ops[]  (96 B: i32 handler, u32 cReg, u32 cLane,
-                  u32 aux, u64 ctrlOut, u64 pad, f64 m[8])
+                  u32 aux, u64 ctrlOut, u64 pad, f64 m[8] / f32 m[16])
 Semantics of every op: src/core/wave.hpp (and the CPU emulation in
 src/cpu/backend_cpu.cpp applyWaveOp, which the tests compare against).
 """
@@ -44,75 +50,85 @@ import os as _os
 # WAVE_ST_POLICY override for experiments, e.g. "" or " sc1"
 LD_POLICY = _os.environ.get("WAVE_LD_POLICY", " nt")
 ST_POLICY = _os.environ.get("WAVE_ST_POLICY", " nt")
-# handler index of the end-of-list sentinel (the last table entry; see
-# idx_slot2 / idx_ph / idx_ch for the kinds after 256)
-OPS_DONE = 532
-# handler table index (shared with the host: backend_hip.hip waveHandlerIndex)
-def idx_slot(kind, s, ctrl):
-    return KINDS.index(kind) * 16 + s * 2 + ctrl          # 0..79
-
-
-def idx_d2s(s, ctrl):
-    return 80 + s * 2 + ctrl                               # 80..95
-
-
-def idx_d2l(ctrl):
-    return 96 + ctrl
-
-
-def idx_tr(s, l):
-    return 100 + s * 6 + l                                 # 100..135
-
-
-def idx_diag(creg, lane):
-    return 136 + creg * 2 + lane                           # 136..(136 + 2^(R+1))
-
-
-# gates applied on lane bits directly (general 2x2 and lane bits >= 3 transpose)
+# ---- handler table (shared with the host through wave_image.inc) ---------
+# gates on lane bits 0-2 directly (no transposition)
 LANE_KINDS, LANE_BITS = ["M2R", "M2RI", "ANTI", "SWAP"], 3
-
-
-def idx_lane(kind, l, ctrl):
-    return 216 + KINDS.index(kind) * 8 + l * 2 + ctrl     # 216..255: gates on lane bits 0-3
-
-
-def idx_trw(s, b):
-    return 200 + s * 4 + b                                 # 200..(200 + 4R), b < 4
-
-
 # cheaper forms of common gates (slot targets): shear rotations (Ry, Rx),
 # the unnormalised Hadamard (its 1/sqrt2 is absorbed by another op of the
 # pass, see src/core/wave.cpp) and Y / -Y as register swaps plus sign flips
 KINDS2 = ["ROTY", "ROTX", "HADD", "YSW", "YSWC"]
-
-
-def idx_slot2(kind, s, ctrl):
-    return 260 + KINDS2.index(kind) * 16 + s * 2 + ctrl    # 260..339
-
-
 # unit-modulus phases on the registers j with (j & creg) == creg (lane = 1:
 # only on lanes whose cLane bits are set): rotation of (re, im) by three
 # shears, negation, multiplication by +-i, negation + rotation
 PH_KINDS = ["DROT", "DNEG", "DMULI", "DMULNI", "DROTN"]
-
-
-def idx_ph(kind, creg, lane):
-    return 340 + PH_KINDS.index(kind) * 32 + creg * 2 + lane  # 340..499 (16 registers)
-
-
 # one-qubit density-matrix channels: a real superoperator on the 4-group of
 # slots (a, b) = (row bit, column bit), g = bit a + 2 bit b: CH1 mixes
 # (x0, x3) by a real 2x2 (m0 m1 / m2 m3) and scales x1, x2 by m4 (dephasing,
 # depolarising, amplitude damping, density collapse); CHD only scales x1, x2
 CH_KINDS = ["CH1", "CHD"]
 
+LAYOUT = {}
+
+
+def set_layout(R):
+    """Base index of every handler family for R register slots; the last
+    entry ("done") is the end-of-list sentinel (the store epilogue)."""
+    NS = 1 << R
+    sizes = [("slot", len(KINDS) * 2 * R), ("d2s", 2 * R), ("d2l", 2), ("tr", 6 * R), ("diag", 2 * NS),
+             ("trw", 4 * R), ("lane", 8 * len(LANE_KINDS)), ("slot2", len(KINDS2) * 2 * R),
+             ("ph", len(PH_KINDS) * 2 * NS), ("ch", len(CH_KINDS) * R * R)]
+    LAYOUT.clear()
+    LAYOUT["R"] = R
+    i = 0
+    for name, n in sizes:
+        LAYOUT[name] = i
+        i += n
+    LAYOUT["done"] = i
+
+
+def idx_slot(kind, s, ctrl):
+    return LAYOUT["slot"] + KINDS.index(kind) * 2 * LAYOUT["R"] + s * 2 + ctrl
+
+
+def idx_d2s(s, ctrl):
+    return LAYOUT["d2s"] + s * 2 + ctrl
+
+
+def idx_d2l(ctrl):
+    return LAYOUT["d2l"] + ctrl
+
+
+def idx_tr(s, l):
+    return LAYOUT["tr"] + s * 6 + l
+
+
+def idx_diag(creg, lane):
+    return LAYOUT["diag"] + creg * 2 + lane
+
+
+def idx_trw(s, b):
+    return LAYOUT["trw"] + s * 4 + b
+
+
+def idx_lane(kind, l, ctrl):
+    return LAYOUT["lane"] + LANE_KINDS.index(kind) * 8 + l * 2 + ctrl
+
+
+def idx_slot2(kind, s, ctrl):
+    return LAYOUT["slot2"] + KINDS2.index(kind) * 2 * LAYOUT["R"] + s * 2 + ctrl
+
+
+def idx_ph(kind, creg, lane):
+    return LAYOUT["ph"] + PH_KINDS.index(kind) * 2 * (1 << LAYOUT["R"]) + creg * 2 + lane
+
 
 def idx_ch(kind, a, b):
-    return 500 + CH_KINDS.index(kind) * 16 + a * 4 + b     # 500..531 (4 slots)
+    return LAYOUT["ch"] + CH_KINDS.index(kind) * LAYOUT["R"] ** 2 + a * LAYOUT["R"] + b
 
 
 def table_size(R):
-    return OPS_DONE + 1
+    set_layout(R)
+    return LAYOUT["done"] + 1
 
 
 _VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b|\b(vcc)\b")
@@ -207,27 +223,31 @@ def schedule(body):
 
 
 class Gen:
-    def __init__(self, R, dbuf, W, debug=False):
+    def __init__(self, R, dbuf, W, P=2, debug=False):
         self.debug = debug
         self.R = R
         self.NS = 1 << R
+        self.P = P               # dwords per value: 2 fp64, 1 fp32
+        self.F = "f64" if P == 2 else "f32"
+        self.MOV = "v_mov_b64" if P == 2 else "v_mov_b32"
+        self.VB = 1 if P == 2 else 2   # tile bits inside one 16-byte vector (slots 0..VB-1)
         self.dbuf = dbuf
         self.W = W               # wave bits: 2^W waves share a tile (LDS exchanges)
         self.NW = 1 << W
-        self.OUTBOX = self.NS * 512   # bytes of one wave's LDS outbox (NS doubles x 64 lanes)
+        self.OUTBOX = self.NS * 64 * 4 * P   # bytes of one wave's LDS outbox (NS values x 64 lanes)
         self.lines = []
-        # v[0 : 4NS) the tile being processed (A), v[4NS : 8NS) the next tile
-        # being loaded (B, software pipeline; dbuf only), then temporaries
-        self.B = 4 * self.NS if dbuf else 0
-        D = (8 if dbuf else 4) * self.NS
+        # v[0 : 2P NS) the tile being processed (A), then the next tile being
+        # loaded (B, software pipeline; dbuf only), then temporaries
+        self.B = 2 * P * self.NS if dbuf else 0
+        D = (2 if dbuf else 1) * 2 * P * self.NS
         self.D = D
-        # 16 temporaries (double pairs): pairs / elements of a handler cycle
+        # 16 temporaries (values): pairs / elements of a handler cycle
         # through 4 / 8 sets so that the scheduler can interleave them
-        self.T = [D + 2 * k for k in range(16)]
-        self.C0, self.C1 = D + 32, D + 34
-        self.vLane, self.vLdB, self.vStB, self.vTmp = D + 36, D + 37, D + 38, D + 39
-        self.CL = D + 40         # 4 doubles: per-lane coefficients of the lane-bit gates
-        self.nvgpr = D + 48      # 112 for R = 4 without the second register set: 4 waves per SIMD
+        self.T = [D + P * k for k in range(16)]
+        self.C0, self.C1 = D + 16 * P, D + 17 * P
+        self.vLane, self.vLdB, self.vStB, self.vTmp = D + 18 * P, D + 18 * P + 1, D + 18 * P + 2, D + 18 * P + 3
+        self.CL = D + 18 * P + 4       # 4 values: per-lane coefficients of the lane-bit gates
+        self.nvgpr = D + 22 * P + 4    # fp64 R = 4: 112 VGPRs, 4 waves per SIMD
         self.handlers = {}
         self.buf = None          # straight-line region being collected for scheduling
 
@@ -252,18 +272,22 @@ class Gen:
         self.lines.append(name + ":")
 
     def re(self, j):
-        return 2 * j
+        return self.P * j
 
     def im(self, j):
-        return 2 * self.NS + 2 * j
+        return self.P * (self.NS + j)
 
-    @staticmethod
-    def vp(r):
-        return f"v[{r}:{r + 1}]"
+    def vp(self, r):
+        return f"v[{r}:{r + 1}]" if self.P == 2 else f"v{r}"
 
-    @staticmethod
-    def sm(k):  # coefficient m[k] (double) in SGPRs
-        return f"s[{76 + 2 * k}:{77 + 2 * k}]"
+    def sm(self, k):  # coefficient m[k] in SGPRs (f64 m[8] / f32 m[16] of the op record)
+        return f"s[{76 + 2 * k}:{77 + 2 * k}]" if self.P == 2 else f"s{76 + k}"
+
+    def op(self, name):  # "fma" -> "v_fma_f64" / "v_fma_f32"
+        return f"v_{name}_{self.F}"
+
+    def hi(self, r):     # dword holding the sign bit of the value at r
+        return r + self.P - 1
 
     def handler(self, idx, name):
         lab = f"wh_{name}"
@@ -347,56 +371,56 @@ class Gen:
         # FMA into its own register (no copies back from temporaries)
         if kind == "M2":
             # T = m01 b, U = m10 a ; a = m00 a + T ; b = m11 b + U
-            e(f"v_mul_f64 {T[0]}, {m(2)}, {r1}")
-            e(f"v_mul_f64 {T[1]}, {m(2)}, {i1}")
-            e(f"v_mul_f64 {T[2]}, {m(4)}, {r0}")
-            e(f"v_mul_f64 {T[3]}, {m(4)}, {i0}")
-            e(f"v_fma_f64 {T[0]}, -{m(3)}, {i1}, {T[0]}")
-            e(f"v_fma_f64 {T[1]}, {m(3)}, {r1}, {T[1]}")
-            e(f"v_fma_f64 {T[2]}, -{m(5)}, {i0}, {T[2]}")
-            e(f"v_fma_f64 {T[3]}, {m(5)}, {r0}, {T[3]}")
-            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i0}, {T[0]}")
-            e(f"v_fma_f64 {T[1]}, {m(1)}, {r0}, {T[1]}")
-            e(f"v_fma_f64 {T[2]}, -{m(7)}, {i1}, {T[2]}")
-            e(f"v_fma_f64 {T[3]}, {m(7)}, {r1}, {T[3]}")
-            e(f"v_fma_f64 {r0}, {m(0)}, {r0}, {T[0]}")
-            e(f"v_fma_f64 {i0}, {m(0)}, {i0}, {T[1]}")
-            e(f"v_fma_f64 {r1}, {m(6)}, {r1}, {T[2]}")
-            e(f"v_fma_f64 {i1}, {m(6)}, {i1}, {T[3]}")
+            e(f"{self.op('mul')} {T[0]}, {m(2)}, {r1}")
+            e(f"{self.op('mul')} {T[1]}, {m(2)}, {i1}")
+            e(f"{self.op('mul')} {T[2]}, {m(4)}, {r0}")
+            e(f"{self.op('mul')} {T[3]}, {m(4)}, {i0}")
+            e(f"{self.op('fma')} {T[0]}, -{m(3)}, {i1}, {T[0]}")
+            e(f"{self.op('fma')} {T[1]}, {m(3)}, {r1}, {T[1]}")
+            e(f"{self.op('fma')} {T[2]}, -{m(5)}, {i0}, {T[2]}")
+            e(f"{self.op('fma')} {T[3]}, {m(5)}, {r0}, {T[3]}")
+            e(f"{self.op('fma')} {T[0]}, -{m(1)}, {i0}, {T[0]}")
+            e(f"{self.op('fma')} {T[1]}, {m(1)}, {r0}, {T[1]}")
+            e(f"{self.op('fma')} {T[2]}, -{m(7)}, {i1}, {T[2]}")
+            e(f"{self.op('fma')} {T[3]}, {m(7)}, {r1}, {T[3]}")
+            e(f"{self.op('fma')} {r0}, {m(0)}, {r0}, {T[0]}")
+            e(f"{self.op('fma')} {i0}, {m(0)}, {i0}, {T[1]}")
+            e(f"{self.op('fma')} {r1}, {m(6)}, {r1}, {T[2]}")
+            e(f"{self.op('fma')} {i1}, {m(6)}, {i1}, {T[3]}")
         elif kind == "M2R":   # m = m00 m01 m10 m11 (real)
-            e(f"v_mul_f64 {T[0]}, {m(1)}, {r1}")
-            e(f"v_mul_f64 {T[1]}, {m(2)}, {r0}")
-            e(f"v_mul_f64 {T[2]}, {m(1)}, {i1}")
-            e(f"v_mul_f64 {T[3]}, {m(2)}, {i0}")
-            e(f"v_fma_f64 {r0}, {m(0)}, {r0}, {T[0]}")
-            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[1]}")
-            e(f"v_fma_f64 {i0}, {m(0)}, {i0}, {T[2]}")
-            e(f"v_fma_f64 {i1}, {m(3)}, {i1}, {T[3]}")
+            e(f"{self.op('mul')} {T[0]}, {m(1)}, {r1}")
+            e(f"{self.op('mul')} {T[1]}, {m(2)}, {r0}")
+            e(f"{self.op('mul')} {T[2]}, {m(1)}, {i1}")
+            e(f"{self.op('mul')} {T[3]}, {m(2)}, {i0}")
+            e(f"{self.op('fma')} {r0}, {m(0)}, {r0}, {T[0]}")
+            e(f"{self.op('fma')} {r1}, {m(3)}, {r1}, {T[1]}")
+            e(f"{self.op('fma')} {i0}, {m(0)}, {i0}, {T[2]}")
+            e(f"{self.op('fma')} {i1}, {m(3)}, {i1}, {T[3]}")
         elif kind == "M2RI":  # m = m00, Im m01, Im m10, m11
             # r0 = m0 r0 - m1 i1 ; i0 = m0 i0 + m1 r1 ; r1 = m3 r1 - m2 i0 ; i1 = m3 i1 + m2 r0
-            e(f"v_mul_f64 {T[0]}, -{m(1)}, {i1}")
-            e(f"v_mul_f64 {T[1]}, {m(1)}, {r1}")
-            e(f"v_mul_f64 {T[2]}, -{m(2)}, {i0}")
-            e(f"v_mul_f64 {T[3]}, {m(2)}, {r0}")
-            e(f"v_fma_f64 {r0}, {m(0)}, {r0}, {T[0]}")
-            e(f"v_fma_f64 {i0}, {m(0)}, {i0}, {T[1]}")
-            e(f"v_fma_f64 {r1}, {m(3)}, {r1}, {T[2]}")
-            e(f"v_fma_f64 {i1}, {m(3)}, {i1}, {T[3]}")
+            e(f"{self.op('mul')} {T[0]}, -{m(1)}, {i1}")
+            e(f"{self.op('mul')} {T[1]}, {m(1)}, {r1}")
+            e(f"{self.op('mul')} {T[2]}, -{m(2)}, {i0}")
+            e(f"{self.op('mul')} {T[3]}, {m(2)}, {r0}")
+            e(f"{self.op('fma')} {r0}, {m(0)}, {r0}, {T[0]}")
+            e(f"{self.op('fma')} {i0}, {m(0)}, {i0}, {T[1]}")
+            e(f"{self.op('fma')} {r1}, {m(3)}, {r1}, {T[2]}")
+            e(f"{self.op('fma')} {i1}, {m(3)}, {i1}, {T[3]}")
         elif kind == "ANTI":  # m = m01 re,im ; m10 re,im
-            e(f"v_mul_f64 {T[0]}, {m(0)}, {r1}")
-            e(f"v_fma_f64 {T[0]}, -{m(1)}, {i1}, {T[0]}")
-            e(f"v_mul_f64 {T[1]}, {m(0)}, {i1}")
-            e(f"v_fma_f64 {T[1]}, {m(1)}, {r1}, {T[1]}")
-            e(f"v_mul_f64 {r1}, {m(2)}, {r0}")
-            e(f"v_fma_f64 {r1}, -{m(3)}, {i0}, {r1}")
-            e(f"v_mul_f64 {i1}, {m(2)}, {i0}")
-            e(f"v_fma_f64 {i1}, {m(3)}, {r0}, {i1}")
-            e(f"v_mov_b64 {r0}, {T[0]}")
-            e(f"v_mov_b64 {i0}, {T[1]}")
+            e(f"{self.op('mul')} {T[0]}, {m(0)}, {r1}")
+            e(f"{self.op('fma')} {T[0]}, -{m(1)}, {i1}, {T[0]}")
+            e(f"{self.op('mul')} {T[1]}, {m(0)}, {i1}")
+            e(f"{self.op('fma')} {T[1]}, {m(1)}, {r1}, {T[1]}")
+            e(f"{self.op('mul')} {r1}, {m(2)}, {r0}")
+            e(f"{self.op('fma')} {r1}, -{m(3)}, {i0}, {r1}")
+            e(f"{self.op('mul')} {i1}, {m(2)}, {i0}")
+            e(f"{self.op('fma')} {i1}, {m(3)}, {r0}, {i1}")
+            e(f"{self.MOV} {r0}, {T[0]}")
+            e(f"{self.MOV} {i0}, {T[1]}")
         elif kind == "SWAP":
             for a, b in ((self.re(j), self.re(f)), (self.im(j), self.im(f))):
-                e(f"v_swap_b32 v{a}, v{b}")
-                e(f"v_swap_b32 v{a + 1}, v{b + 1}")
+                for d in range(self.P):
+                    e(f"v_swap_b32 v{a + d}, v{b + d}")
         elif kind == "ROTY":   # (a, b) -> (c a - s b, s a + c b) on re and im: m = tan(phi/2), sin(phi)
             for base in (self.re, self.im):
                 self.rot(base(j), base(f), False)
@@ -406,16 +430,16 @@ class Gen:
         elif kind == "HADD":   # (a, b) -> (a + b, a - b), unnormalised
             for base in (self.re, self.im):
                 a, b = self.vp(base(j)), self.vp(base(f))
-                e(f"v_add_f64 {b}, {a}, -{b}")
-                e(f"v_fma_f64 {a}, 2.0, {a}, -{b}")
+                e(f"{self.op('add')} {b}, {a}, -{b}")
+                e(f"{self.op('fma')} {a}, 2.0, {a}, -{b}")
         elif kind in ("YSW", "YSWC"):
             # Y: a -> -i b, b -> i a  (YSWC: -Y): swap a_re <-> b_im, a_im <-> b_re, then two sign flips
             for x, y in ((self.re(j), self.im(f)), (self.im(j), self.re(f))):
-                e(f"v_swap_b32 v{x}, v{y}")
-                e(f"v_swap_b32 v{x + 1}, v{y + 1}")
+                for d in range(self.P):
+                    e(f"v_swap_b32 v{x + d}, v{y + d}")
             neg = (self.im(j), self.re(f)) if kind == "YSW" else (self.re(j), self.im(f))
             for r in neg:
-                e(f"v_xor_b32_e32 v{r + 1}, 0x80000000, v{r + 1}")
+                e(f"v_xor_b32_e32 v{self.hi(r)}, 0x80000000, v{self.hi(r)}")
         else:
             raise ValueError(kind)
 
@@ -426,26 +450,26 @@ class Gen:
         t, sn = self.sm(0), self.sm(1)
         mt, ps = (t, "-" + sn) if neg else ("-" + t, sn)
         X, Y = self.vp(x), self.vp(y)
-        self.e(f"v_fma_f64 {X}, {mt}, {Y}, {X}")
-        self.e(f"v_fma_f64 {Y}, {ps}, {X}, {Y}")
-        self.e(f"v_fma_f64 {X}, {mt}, {Y}, {X}")
+        self.e(f"{self.op('fma')} {X}, {mt}, {Y}, {X}")
+        self.e(f"{self.op('fma')} {Y}, {ps}, {X}, {Y}")
+        self.e(f"{self.op('fma')} {X}, {mt}, {Y}, {X}")
 
     def cmul_sgpr(self, j, kr, ki, ts=0):
         # (x + iy) *= (m[kr] + i m[ki])
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
         T = [self.vp(t) for t in self.T[2 * ts:2 * ts + 2]]
-        self.e(f"v_mul_f64 {T[0]}, {self.sm(ki)}, {y}")
-        self.e(f"v_mul_f64 {T[1]}, {self.sm(ki)}, {x}")
-        self.e(f"v_fma_f64 {x}, {self.sm(kr)}, {x}, -{T[0]}")
-        self.e(f"v_fma_f64 {y}, {self.sm(kr)}, {y}, {T[1]}")
+        self.e(f"{self.op('mul')} {T[0]}, {self.sm(ki)}, {y}")
+        self.e(f"{self.op('mul')} {T[1]}, {self.sm(ki)}, {x}")
+        self.e(f"{self.op('fma')} {x}, {self.sm(kr)}, {x}, -{T[0]}")
+        self.e(f"{self.op('fma')} {y}, {self.sm(kr)}, {y}, {T[1]}")
 
     def cmul_vgpr(self, j, cr, ci, ts=0):
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
         T = [self.vp(t) for t in self.T[2 * ts:2 * ts + 2]]
-        self.e(f"v_mul_f64 {T[0]}, {self.vp(ci)}, {y}")
-        self.e(f"v_mul_f64 {T[1]}, {self.vp(ci)}, {x}")
-        self.e(f"v_fma_f64 {x}, {self.vp(cr)}, {x}, -{T[0]}")
-        self.e(f"v_fma_f64 {y}, {self.vp(cr)}, {y}, {T[1]}")
+        self.e(f"{self.op('mul')} {T[0]}, {self.vp(ci)}, {y}")
+        self.e(f"{self.op('mul')} {T[1]}, {self.vp(ci)}, {x}")
+        self.e(f"{self.op('fma')} {x}, {self.vp(cr)}, {x}, -{T[0]}")
+        self.e(f"{self.op('fma')} {y}, {self.vp(cr)}, {y}, {T[1]}")
 
     # ---- handlers --------------------------------------------------------
     def gen_slot(self, kind, s, ctrl):
@@ -504,15 +528,15 @@ class Gen:
         for j in [j for j in range(self.NS) if (j & creg) == creg]:
             x, y = self.re(j), self.im(j)
             if kind in ("DNEG", "DROTN"):
-                e(f"v_xor_b32_e32 v{x + 1}, 0x80000000, v{x + 1}")
-                e(f"v_xor_b32_e32 v{y + 1}, 0x80000000, v{y + 1}")
+                e(f"v_xor_b32_e32 v{self.hi(x)}, 0x80000000, v{self.hi(x)}")
+                e(f"v_xor_b32_e32 v{self.hi(y)}, 0x80000000, v{self.hi(y)}")
             if kind in ("DROT", "DROTN"):
                 self.rot(x, y, False)
             elif kind in ("DMULI", "DMULNI"):   # x + iy -> -y + ix  /  y - ix
-                e(f"v_swap_b32 v{x}, v{y}")
-                e(f"v_swap_b32 v{x + 1}, v{y + 1}")
+                for d in range(self.P):
+                    e(f"v_swap_b32 v{x + d}, v{y + d}")
                 r = x if kind == "DMULI" else y
-                e(f"v_xor_b32_e32 v{r + 1}, 0x80000000, v{r + 1}")
+                e(f"v_xor_b32_e32 v{self.hi(r)}, 0x80000000, v{self.hi(r)}")
         self.end_region()
         if lane:
             e("s_mov_b64 exec, -1")
@@ -529,15 +553,15 @@ class Gen:
             x = [j, j | (1 << a), j | (1 << b), j | (1 << a) | (1 << b)]
             for base in (self.re, self.im):
                 X = [self.vp(base(r)) for r in x]
-                e(f"v_mul_f64 {X[1]}, {self.sm(4)}, {X[1]}")
-                e(f"v_mul_f64 {X[2]}, {self.sm(4)}, {X[2]}")
+                e(f"{self.op('mul')} {X[1]}, {self.sm(4)}, {X[1]}")
+                e(f"{self.op('mul')} {X[2]}, {self.sm(4)}, {X[2]}")
                 if kind == "CH1":
                     T = self.vp(self.T[k % 16])
                     k += 1
-                    e(f"v_mul_f64 {T}, {self.sm(2)}, {X[0]}")
-                    e(f"v_mul_f64 {X[0]}, {self.sm(0)}, {X[0]}")
-                    e(f"v_fma_f64 {X[0]}, {self.sm(1)}, {X[3]}, {X[0]}")
-                    e(f"v_fma_f64 {X[3]}, {self.sm(3)}, {X[3]}, {T}")
+                    e(f"{self.op('mul')} {T}, {self.sm(2)}, {X[0]}")
+                    e(f"{self.op('mul')} {X[0]}, {self.sm(0)}, {X[0]}")
+                    e(f"{self.op('fma')} {X[0]}, {self.sm(1)}, {X[3]}, {X[0]}")
+                    e(f"{self.op('fma')} {X[3]}, {self.sm(3)}, {X[3]}, {T}")
         self.end_region()
         self.back()
 
@@ -568,13 +592,13 @@ class Gen:
         self.e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, s71, 1")
         self.e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
         C0, C1, T0, T1 = self.C0, self.C1, self.T[14], self.T[15]
-        self.e(f"v_mov_b64 {self.vp(C0)}, {self.sm(0)}")
-        self.e(f"v_mov_b64 {self.vp(C1)}, {self.sm(1)}")
-        self.e(f"v_mov_b64 {self.vp(T0)}, {self.sm(2)}")
-        self.e(f"v_mov_b64 {self.vp(T1)}, {self.sm(3)}")
+        self.e(f"{self.MOV} {self.vp(C0)}, {self.sm(0)}")
+        self.e(f"{self.MOV} {self.vp(C1)}, {self.sm(1)}")
+        self.e(f"{self.MOV} {self.vp(T0)}, {self.sm(2)}")
+        self.e(f"{self.MOV} {self.vp(T1)}, {self.sm(3)}")
         for c, t in ((C0, T0), (C1, T1)):
-            self.e(f"v_cndmask_b32_e32 v{c}, v{c}, v{t}, vcc")
-            self.e(f"v_cndmask_b32_e32 v{c + 1}, v{c + 1}, v{t + 1}, vcc")
+            for d in range(self.P):
+                self.e(f"v_cndmask_b32_e32 v{c + d}, v{c + d}, v{t + d}, vcc")
         if ctrl:
             self.ctrl_begin()
         else:
@@ -610,13 +634,17 @@ class Gen:
         C0, C1 = self.C0, self.C1
         e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
         e(f"v_cmp_eq_u32_e32 vcc, s70, v{self.vTmp}")
-        e(f"v_mov_b64 {self.vp(C0)}, {self.sm(0)}")
-        e(f"v_mov_b64 {self.vp(C1)}, {self.sm(1)}")
-        e(f"v_cndmask_b32_e32 v{C0}, 0, v{C0}, vcc")
-        e(f"v_mov_b32_e32 v{self.vTmp}, 0x3ff00000")   # hi dword of 1.0 (literal + vcc: two constant-bus reads)
-        e(f"v_cndmask_b32_e32 v{C0 + 1}, v{self.vTmp}, v{C0 + 1}, vcc")
-        e(f"v_cndmask_b32_e32 v{C1}, 0, v{C1}, vcc")
-        e(f"v_cndmask_b32_e32 v{C1 + 1}, 0, v{C1 + 1}, vcc")
+        e(f"{self.MOV} {self.vp(C0)}, {self.sm(0)}")
+        e(f"{self.MOV} {self.vp(C1)}, {self.sm(1)}")
+        if self.P == 2:
+            e(f"v_cndmask_b32_e32 v{C0}, 0, v{C0}, vcc")
+            e(f"v_mov_b32_e32 v{self.vTmp}, 0x3ff00000")   # hi dword of 1.0 (literal + vcc: two constant-bus reads)
+            e(f"v_cndmask_b32_e32 v{C0 + 1}, v{self.vTmp}, v{C0 + 1}, vcc")
+            e(f"v_cndmask_b32_e32 v{C1}, 0, v{C1}, vcc")
+            e(f"v_cndmask_b32_e32 v{C1 + 1}, 0, v{C1 + 1}, vcc")
+        else:
+            e(f"v_cndmask_b32_e32 v{C0}, 1.0, v{C0}, vcc")
+            e(f"v_cndmask_b32_e32 v{C1}, 0, v{C1}, vcc")
         self.region()
         for k, j in enumerate(js):
             self.cmul_vgpr(j, C0, C1, k % 8)
@@ -633,9 +661,9 @@ class Gen:
                 continue
             f = j | (1 << s)
             for base in (self.re, self.im):
-                pairs.append((base(j), base(f)))
-                pairs.append((base(j) + 1, base(f) + 1))
-        tmp = [self.T[0], self.T[0] + 1, self.T[1], self.T[1] + 1, self.T[2], self.T[2] + 1, self.T[3], self.T[3] + 1]
+                for d in range(self.P):
+                    pairs.append((base(j) + d, base(f) + d))
+        tmp = [self.D + i for i in range(8)]   # the first 8 dwords of the temporaries
         if l >= 4:
             op = "v_permlane32_swap_b32_e32" if l == 5 else "v_permlane16_swap_b32_e32"
             for a, b in pairs:
@@ -648,9 +676,10 @@ class Gen:
             hi_banks = "0xc" if l == 3 else "0xa"   # lanes with the bit set
             # all copies first (32 temporaries), then the DPP moves: one
             # VALU-write -> DPP-read wait for the whole handler
-            big = [self.T[0] + i for i in range(32)]
-            for g in range(0, len(pairs), 32):
-                grp = pairs[g:g + 32]
+            G = 16 * self.P                    # dwords of temporaries
+            big = [self.D + i for i in range(G)]
+            for g in range(0, len(pairs), G):
+                grp = pairs[g:g + G]
                 for k, (a, b) in enumerate(grp):
                     e(f"v_mov_b32_e32 v{big[k]}, v{b}")
                 e("s_nop 1")
@@ -696,54 +725,55 @@ class Gen:
         CL, C0 = self.CL, self.C0
 
         def sel(dst, k_clear, k_set):
-            e(f"v_mov_b64 {self.vp(dst)}, {self.sm(k_clear)}")
-            e(f"v_mov_b64 {self.vp(C0)}, {self.sm(k_set)}")
-            e(f"v_cndmask_b32_e32 v{dst}, v{dst}, v{C0}, vcc")
-            e(f"v_cndmask_b32_e32 v{dst + 1}, v{dst + 1}, v{C0 + 1}, vcc")
+            e(f"{self.MOV} {self.vp(dst)}, {self.sm(k_clear)}")
+            e(f"{self.MOV} {self.vp(C0)}, {self.sm(k_set)}")
+            for d in range(self.P):
+                e(f"v_cndmask_b32_e32 v{dst + d}, v{dst + d}, v{C0 + d}, vcc")
+        P = self.P
         if kind in ("M2R", "M2RI"):      # m00 m01 m10 m11 (M2RI: the off-diagonals imaginary)
             sel(CL, 0, 3)
-            sel(CL + 2, 1, 2)
+            sel(CL + P, 1, 2)
         elif kind == "ANTI":             # m01 re,im ; m10 re,im
-            sel(CL + 4, 0, 2)
-            sel(CL + 6, 1, 3)
+            sel(CL + 2 * P, 0, 2)
+            sel(CL + 3 * P, 1, 3)
         elif kind == "M2":               # m00, m01, m10, m11 complex
             sel(CL, 0, 6)
-            sel(CL + 2, 1, 7)
-            sel(CL + 4, 2, 4)
-            sel(CL + 6, 3, 5)
+            sel(CL + P, 1, 7)
+            sel(CL + 2 * P, 2, 4)
+            sel(CL + 3 * P, 3, 5)
 
     def lane_math(self, kind, j, px, py, B=None):
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
-        CS, CP = self.vp(self.CL), self.vp(self.CL + 2)
-        CSr, CSi, CPr, CPi = (self.vp(self.CL + 2 * k) for k in range(4))
+        CS, CP = self.vp(self.CL), self.vp(self.CL + self.P)
+        CSr, CSi, CPr, CPi = (self.vp(self.CL + self.P * k) for k in range(4))
         e = self.e
         px, py = self.vp(px), self.vp(py)
         if kind == "M2R":
-            e(f"v_mul_f64 {px}, {CP}, {px}")
-            e(f"v_mul_f64 {py}, {CP}, {py}")
-            e(f"v_fma_f64 {x}, {CS}, {x}, {px}")
-            e(f"v_fma_f64 {y}, {CS}, {y}, {py}")
+            e(f"{self.op('mul')} {px}, {CP}, {px}")
+            e(f"{self.op('mul')} {py}, {CP}, {py}")
+            e(f"{self.op('fma')} {x}, {CS}, {x}, {px}")
+            e(f"{self.op('fma')} {y}, {CS}, {y}, {py}")
         elif kind == "M2RI":
-            e(f"v_mul_f64 {py}, -{CP}, {py}")
-            e(f"v_mul_f64 {px}, {CP}, {px}")
-            e(f"v_fma_f64 {x}, {CS}, {x}, {py}")
-            e(f"v_fma_f64 {y}, {CS}, {y}, {px}")
+            e(f"{self.op('mul')} {py}, -{CP}, {py}")
+            e(f"{self.op('mul')} {px}, {CP}, {px}")
+            e(f"{self.op('fma')} {x}, {CS}, {x}, {py}")
+            e(f"{self.op('fma')} {y}, {CS}, {y}, {px}")
         elif kind == "ANTI":
-            CPr, CPi = self.vp(self.CL + 4), self.vp(self.CL + 6)
-            e(f"v_mul_f64 {x}, {CPr}, {px}")
-            e(f"v_mul_f64 {y}, {CPr}, {py}")
-            e(f"v_fma_f64 {x}, -{CPi}, {py}, {x}")
-            e(f"v_fma_f64 {y}, {CPi}, {px}, {y}")
+            CPr, CPi = self.vp(self.CL + 2 * self.P), self.vp(self.CL + 3 * self.P)
+            e(f"{self.op('mul')} {x}, {CPr}, {px}")
+            e(f"{self.op('mul')} {y}, {CPr}, {py}")
+            e(f"{self.op('fma')} {x}, -{CPi}, {py}, {x}")
+            e(f"{self.op('fma')} {y}, {CPi}, {px}, {y}")
         elif kind == "M2":
             B = self.vp(B)
-            e(f"v_mul_f64 {B}, {CPr}, {py}")
-            e(f"v_fma_f64 {B}, {CPi}, {px}, {B}")
-            e(f"v_mul_f64 {px}, {CPr}, {px}")
-            e(f"v_fma_f64 {px}, -{CPi}, {py}, {px}")
-            e(f"v_fma_f64 {px}, -{CSi}, {y}, {px}")
-            e(f"v_fma_f64 {B}, {CSi}, {x}, {B}")
-            e(f"v_fma_f64 {x}, {CSr}, {x}, {px}")
-            e(f"v_fma_f64 {y}, {CSr}, {y}, {B}")
+            e(f"{self.op('mul')} {B}, {CPr}, {py}")
+            e(f"{self.op('fma')} {B}, {CPi}, {px}, {B}")
+            e(f"{self.op('mul')} {px}, {CPr}, {px}")
+            e(f"{self.op('fma')} {px}, -{CPi}, {py}, {px}")
+            e(f"{self.op('fma')} {px}, -{CSi}, {y}, {px}")
+            e(f"{self.op('fma')} {B}, {CSi}, {x}, {B}")
+            e(f"{self.op('fma')} {x}, {CSr}, {x}, {px}")
+            e(f"{self.op('fma')} {y}, {CSr}, {y}, {B}")
 
     def gen_lane(self, kind, l, ctrl):
         """A one-qubit gate whose target is lane bit l: every lane combines
@@ -767,12 +797,12 @@ class Gen:
                 self.ctrl_j(j0, skip)
             if kind == "SWAP":
                 for j in js:
-                    regs = [self.re(j), self.re(j) + 1, self.im(j), self.im(j) + 1]
+                    regs = [self.re(j) + d for d in range(self.P)] + [self.im(j) + d for d in range(self.P)]
                     if l < 2:
                         for r in regs:   # in place: DPP reads every lane before writing
                             self.lane_fetch(l, r, r)
                     else:
-                        tmp = [self.T[0] + k for k in range(4)]
+                        tmp = [self.D + k for k in range(2 * self.P)]
                         for r, t in zip(regs, tmp):
                             e(f"v_mov_b32_e32 v{t}, v{r}")
                         e("s_nop 1")
@@ -783,7 +813,7 @@ class Gen:
                 for k, j in enumerate(js):
                     px, py = self.T[per * k], self.T[per * k + 1]
                     B = self.T[per * k + 2] if kind == "M2" else None
-                    for d in (0, 1):
+                    for d in range(self.P):
                         self.lane_fetch(l, px + d, self.re(j) + d)
                         self.lane_fetch(l, py + d, self.im(j) + d)
                     slots.append((j, px, py, B))
@@ -815,7 +845,7 @@ class Gen:
             hi_regs += [self.re(j), self.im(j)]
         ob = self.OUTBOX
         e(f"s_mul_i32 s96, s3, {ob}")
-        e(f"v_lshlrev_b32_e32 v{vt}, 3, v{vl}")
+        e(f"v_lshlrev_b32_e32 v{vt}, {2 if self.P == 1 else 3}, v{vl}")
         e(f"v_add_u32_e32 v{vt}, s96, v{vt}")
         for phase in ("w", "r"):
             e(f"s_bitcmp1_b32 s3, {b}")
@@ -824,10 +854,11 @@ class Gen:
                 if tag == "hi":
                     self.label(f".Ltrw_{s}_{b}_{phase}hi")
                 for k, r in enumerate(regs):
+                    stride = 256 * self.P
                     if phase == "w":
-                        e(f"ds_write_b64 v{vt}, v[{r}:{r + 1}] offset:{k * 512}")
+                        e(f"ds_write_b{32 * self.P} v{vt}, {self.vp(r)} offset:{k * stride}")
                     else:
-                        e(f"ds_read_b64 v[{r}:{r + 1}], v{vt} offset:{k * 512}")
+                        e(f"ds_read_b{32 * self.P} {self.vp(r)}, v{vt} offset:{k * stride}")
                 if tag == "lo":
                     e(f"s_branch .Ltrw_{s}_{b}_{phase}done")
             self.label(f".Ltrw_{s}_{b}_{phase}done")
@@ -840,7 +871,7 @@ class Gen:
     # ---- the kernel -------------------------------------------------------
     def kernel(self):
         R, NS, D = self.R, self.NS, self.D
-        NG = NS // 2       # 16-byte groups per array per lane
+        NG = NS * self.P // 4   # 16-byte groups per array per lane
         K = R + 6 + self.W  # tile bits
         L = self.lines
         L.append('\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"')
@@ -942,7 +973,7 @@ class Gen:
             self.label(".Ltile_loop")
             e(f"s_waitcnt vmcnt({2 * NG})")   # tile i+1's loads are older than tile i's stores
             self.label(".Lcopy")
-            for r in range(0, 4 * NS, 2):
+            for r in range(0, 2 * self.P * NS, 2):
                 e(f"v_mov_b64 v[{r}:{r + 1}], v[{self.B + r}:{self.B + r + 1}]")
             self.base_of("s[16:17]", 32)     # this tile: ctrlOut tests and stores
             # prefetch the next tile into B
@@ -969,7 +1000,7 @@ class Gen:
         self.next_op()
         self.check_path()
         self.label("wh_OPS_DONE")     # the sentinel record's handler
-        self.handlers[OPS_DONE] = "wh_OPS_DONE"
+        self.handlers[LAYOUT["done"]] = "wh_OPS_DONE"
         e("s_waitcnt lgkmcnt(0)")      # the prefetch past the last op writes s[36:59]
         self.wave_bytes(ST_WAVE, 34)
         self.groups("st", 216, vstb, NG, 0, 96)
@@ -1009,7 +1040,6 @@ class Gen:
                     if kind == "HADD" and c:
                         continue   # only uncontrolled Hadamards drop their 1/sqrt2
                     self.gen_slot2(kind, s, c)
-        assert NS <= 16 and R <= 4, "idx_ph reserves 32 entries per phase kind, idx_ch 16 per channel kind"
         for kind in CH_KINDS:
             for a in range(R):
                 for b in range(R):
@@ -1082,7 +1112,7 @@ class Gen:
         q = 0
         for jj in range(NG):
             g = (52 + 2 * jj) if jj < 8 else (68 + 2 * (jj - 8))
-            for arr, base in ((4, regbase + 2 * jj * 2), (6, regbase + 2 * self.NS + 2 * jj * 2)):
+            for arr, base in ((4, regbase + 4 * jj), (6, regbase + self.P * self.NS + 4 * jj)):
                 Q = (36, 40, 44, 48)[q % 4]
                 q += 1
                 e(f"s_add_u32 s{Q}, s{arr}, s{bpair}")
@@ -1190,6 +1220,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("mode", choices=["asm", "embed"])
     ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--prec", type=int, default=2, choices=[1, 2], help="QuEST_PREC: 2 fp64, 1 fp32")
     ap.add_argument("--dbuf", type=int, default=-1, help="software-pipelined tiles (default: when 4 slots)")
     ap.add_argument("--wbits", type=int, default=3, help="2^wbits waves share a tile")
     ap.add_argument("--debug", action="store_true", help="record addressing state per wave and stop (no state access)")
@@ -1201,7 +1232,8 @@ def main():
         # the second register set costs a wave per SIMD: worth it only while
         # a tile has <= 4 waves (otherwise too few workgroups fit a CU)
         dbuf = args.dbuf if args.dbuf >= 0 else (args.slots <= 4 and args.wbits <= 2)
-        g = Gen(args.slots, dbuf, args.wbits, args.debug)
+        set_layout(args.slots)
+        g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug)
         g.kernel()
         with open(args.out, "w") as f:
             f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
@@ -1224,7 +1256,11 @@ def main():
         f.write(f"static const int kWaveImageWBits = {args.wbits};\n")
         vg = re.search(r"amdhsa_next_free_vgpr (\d+)", open(args.out.replace("wave_image.inc", "wave_kernel.s")).read())
         f.write(f"static const int kWaveImageVgprs = {vg.group(1)};\n")
-        f.write(f"static const int kWaveSentinelIndex = {OPS_DONE};\n")
+        set_layout(args.slots)
+        f.write(f"static const int kWaveImagePrec = {args.prec};\n")
+        for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch"):
+            f.write(f"static const int kWaveIdx_{k} = {LAYOUT[k]};\n")
+        f.write(f"static const int kWaveSentinelIndex = {LAYOUT['done']};\n")
         f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
         f.write(f"static const unsigned char kWaveImage[{len(img)}] __attribute__((aligned(4096))) = {{\n")
         for k in range(0, len(img), 24):
