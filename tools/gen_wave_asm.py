@@ -1092,7 +1092,7 @@ class Gen:
             e(f"s_add_u32 s94, {p}, 1")
             e(f"s_lshl_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s94")
             e(f"s_or_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s[98:99]")
-        e(f"s_lshl_b64 s[{d + 2}:{d + 3}], s[{d}:{d + 1}], 3")
+        e(f"s_lshl_b64 s[{d + 2}:{d + 3}], s[{d}:{d + 1}], {3 if self.P == 2 else 2}")   # bytes
 
     def groups(self, what, off, vb, NG, regbase, bpair):
         """Load or store the NG 16-byte groups of re and im (per lane) of the

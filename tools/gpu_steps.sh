@@ -12,6 +12,11 @@ for spec in "$@"; do
     rc=$?
     echo "=== $name rc=$rc $(( $(date +%s) - start )) s"
     tail -5 "gpurun_out/$name.log"
+    # a device fault inside a test (pytest exit 1) ends the script as well
+    if grep -q -E "illegal memory access|Memory access fault|HIP error|hipError|GPU fault" "gpurun_out/$name.log"; then
+        echo "=== stopping after $name: device fault in the log"
+        exit 3
+    fi
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
         echo "=== stopping after $name (rc=$rc)"
         exit $rc
