@@ -26,6 +26,7 @@
 #include "../core/backend.hpp"
 #include "../core/router.hpp"
 #include "../core/tiles.hpp"
+#include "../core/wave.hpp"
 #include "common.hpp"
 #include "qasm.hpp"
 #include "validation.hpp"
@@ -932,6 +933,10 @@ int setQuESTTuning(const char* key, int value) {
         rt().verify = value != 0;
         return 1;
     }
+    if (key && !strcmp(key, "wave_relabel")) {
+        waveRelabel() = value != 0;
+        return 1;
+    }
     if (key && !strcmp(key, "verify_inject")) {  // fault injection for the verify test
         rt().verifyInject = value != 0;
         return 1;
@@ -946,6 +951,8 @@ int getQuESTTuning(const char* key, int* value) {
         v = fuseBlocks() ? 1 : 0;
     else if (key && !strcmp(key, "verify"))
         v = rt().verify ? 1 : 0;
+    else if (key && !strcmp(key, "wave_relabel"))
+        v = waveRelabel() ? 1 : 0;
     else
         known = be::getTuning(key, &v);
     if (known && value) *value = v;

@@ -30,6 +30,7 @@ void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k,
         tileOf[bit] = -1;
         if ((q >> bit) & 1) {
             tileOf[bit] = n;
+            ps.stPos[n] = bit;
             ps.pos[n++] = bit;
         }
     }
@@ -373,9 +374,92 @@ void fuseGates(std::vector<Op>& ops) {
     ops.swap(out);
 }
 
-void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out) {
+bool programRelabels(const TileProgram& prog) {
+    for (const TilePass& ps : prog.passes)
+        for (int i = 0; i < ps.k; i++)
+            if (ps.stPos[i] != ps.pos[i]) return true;
+    return false;
+}
+
+namespace {
+
+// Permute physical positions of an op by pi (positions not in pi unchanged).
+void remapOp(Op& op, const int* pi) {
+    for (int j = 0; j < op.nt; j++) op.t[j] = pi[op.t[j]];
+    u64 c = 0;
+    for (u64 m = op.ctrl; m; m &= m - 1) c |= 1ull << pi[__builtin_ctzll(m)];
+    op.ctrl = c;
+}
+
+// Choose the store permutation of the pass just emitted (out.passes.back())
+// and apply it to the ops not yet scheduled.  The tile's positions >= from
+// hold some logical qubits; the ones the queue needs soonest (first op
+// targeting them) take the low positions [from, c), which every later tile
+// contains; the qubits they displace take the vacated high positions.
+void relabelPass(std::vector<Op>& ops, const std::vector<char>& done, int first, int from, int c, int L,
+                 TileProgram& out) {
+    TilePass& ps = out.passes.back();
+    const int INF = 1 << 30;
+    int need[64];
+    for (int p = 0; p < 64; p++) need[p] = INF;
+    u64 open = 0;
+    for (int i = 0; i < ps.k; i++) open |= 1ull << ps.pos[i];
+    for (int i = first, rank = 0; i < (int)ops.size() && open; i++) {
+        if (done[i]) continue;
+        u64 tg = targetMask(ops[i]) & open;
+        for (; tg; tg &= tg - 1) {
+            const int p = __builtin_ctzll(tg);
+            need[p] = rank;
+            open &= ~(1ull << p);
+        }
+        rank++;
+    }
+    std::vector<int> cand;
+    for (int i = 0; i < ps.k; i++)
+        if (ps.pos[i] >= from) cand.push_back(ps.pos[i]);
+    // soonest first; among equals keep the qubits already low
+    std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) {
+        if (need[a] != need[b]) return need[a] < need[b];
+        return (a < c) > (b < c);
+    });
+    const int slots = c - from;
+    std::vector<int> in, freeLow;
+    std::vector<char> chosenLow(64, 0);
+    for (int x = 0; x < slots && x < (int)cand.size(); x++) {
+        if (need[cand[x]] == INF) break;
+        if (cand[x] < c)
+            chosenLow[cand[x]] = 1;
+        else
+            in.push_back(cand[x]);
+    }
+    for (int p = from; p < c; p++)
+        if (!chosenLow[p]) freeLow.push_back(p);
+    // the low qubits needed latest make room first
+    std::stable_sort(freeLow.begin(), freeLow.end(), [&](int a, int b) { return need[a] > need[b]; });
+    int pi[64];
+    for (int p = 0; p < 64; p++) pi[p] = p;
+    bool any = false;
+    for (size_t x = 0; x < in.size() && x < freeLow.size(); x++) {
+        const int hi = in[x], lo = freeLow[x];
+        if (need[lo] <= need[hi]) continue;
+        pi[hi] = lo;
+        pi[lo] = hi;
+        any = true;
+    }
+    if (!any) return;
+    for (int i = 0; i < ps.k; i++) ps.stPos[i] = pi[ps.pos[i]];
+    for (int i = first; i < (int)ops.size(); i++)
+        if (!done[i]) remapOp(ops[i], pi);
+    for (int x = 0; x < L; x++) out.perm[x] = pi[out.perm[x]];
+}
+
+}  // namespace
+
+void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom) {
     out.passes.clear();
     out.ops.clear();
+    out.perm.resize(L);
+    for (int x = 0; x < L; x++) out.perm[x] = x;
     if (ops.empty()) return;
     const int k = std::min(kmax, L);
     const int c = std::min(cmin, k);
@@ -487,6 +571,8 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             done[i] = 1;
         }
         emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out);
+        if (relabelFrom >= 0 && (int)best.size() >= 2 && (int)order.size() < n)
+            relabelPass(ops, done, first, relabelFrom, c, L, out);
     }
     ops.swap(order);
 }

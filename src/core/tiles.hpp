@@ -83,6 +83,10 @@ inline unsigned ldsSwizzle(unsigned p) { return p ^ ldsSwizzleHash(p >> 5); }
 struct TilePass {
     int k = 0;           // tile qubits
     int pos[32];         // tile bit i -> physical bit position (ascending)
+    // tile bit -> physical position it is STORED to: a permutation of pos
+    // when the pass relabels qubits in place (planTiles relabelFrom >= 0);
+    // later passes and the register's qubit map follow the new layout
+    int stPos[32];
     u64 qmask = 0;       // physical mask of Q
     int opBegin = 0;     // range in the program's op array
     int opEnd = 0;
@@ -92,6 +96,9 @@ struct TilePass {
 
 struct TileProgram {
     std::vector<TilePass> passes;
+    // physical position at the start of the program -> position at its end
+    // (identity unless passes relabel); size L
+    std::vector<int> perm;
     std::vector<TileOp> ops;
     std::vector<TilePhase> phases;
     // dense block matrices: 2^R x 2^R complex, row-major, interleaved re/im
@@ -126,7 +133,15 @@ int& fuseBlockQubits();
 // most kmax tile qubits (kmax >= cmin + 4).  With fuse=true ops are reordered
 // where they commute to fill each pass (`ops` is left in execution order);
 // with fuse=false every op gets its own pass, in order.
-void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out);
+//
+// relabelFrom >= 0 (wave engine): a pass of two or more ops may store its
+// tile with the qubits permuted among the tile's positions >= relabelFrom,
+// so that the qubits the rest of the queue needs soonest land on the low
+// positions below cmin, which every later tile contains.  The remaining ops
+// are remapped to the new layout and out.perm records the composition.
+void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1);
+// Whether any pass of the program stores with a permuted layout.
+bool programRelabels(const TileProgram& prog);
 
 // Physical chunk index of element p of tile T in a pass.
 inline i64 tileBase(const TilePass& ps, i64 T, int L) {

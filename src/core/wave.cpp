@@ -185,6 +185,38 @@ void settleScale(WaveProgram& out, int begin, double sr, double si) {
     out.ops.push_back(w);
 }
 
+bool& waveRelabel() {
+    static bool on = !getenv("QUEST_WAVE_RELABEL") || atoi(getenv("QUEST_WAVE_RELABEL")) != 0;
+    return on;
+}
+
+bool relabelsLower(const TileProgram& prog) {
+    const Stats keep = stats();
+    bool ok = true;
+    for (const TilePass& ps : prog.passes) {
+        bool perm = false;
+        for (int i = 0; i < ps.k; i++) perm |= ps.stPos[i] != ps.pos[i];
+        if (!perm) continue;
+        WaveProgram tmp;
+        if (!planWavePass(ps, prog.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, tmp)) {
+            ok = false;
+            break;
+        }
+    }
+    stats() = keep;
+    return ok;
+}
+
+void applyProgramPerm(QuregImpl& q, const TileProgram& prog) {
+    if ((int)prog.perm.size() != q.L) return;
+    bool id = true;
+    for (int x = 0; x < q.L; x++) id = id && prog.perm[x] == x;
+    if (id) return;
+    for (int lg = 0; lg < q.nSV; lg++)
+        if (q.l2p[lg] < q.L) q.l2p[lg] = prog.perm[q.l2p[lg]];
+    for (int lg = 0; lg < q.nSV; lg++) q.p2l[q.l2p[lg]] = lg;
+}
+
 int waveTransposeCost(int laneBit) { return laneBit >= kWaveLanes ? 3 : laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
 
 bool waveChannel(const real* m) {
@@ -247,7 +279,13 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     auto laneOpsMax = [&](int b) { return !laneOps ? 0 : (b >= 1 && b <= 3) ? 4 : 2; };
 
     WavePass wp;
-    for (int i = 0; i < kWaveBits; i++) wp.pos[i] = ps.pos[i];
+    for (int i = 0; i < kWaveBits; i++) {
+        wp.pos[i] = ps.pos[i];
+        wp.stPos[i] = ps.stPos[i];
+    }
+    // the vector bits never move (no slot-0 transpositions)
+    for (int v = 0; v < kWaveVecBits; v++)
+        if (ps.stPos[v] != v) return false;
     // load layout: the vector bits (fp64: tile bit 0, fp32: bits 0-1) in
     // slots 0.., the next three on lanes 0-2 (8 lanes x 16 bytes = one 128-byte
     // line); of the higher tile bits those needed in a slot earliest take the
@@ -557,10 +595,16 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         out.ops.push_back(w);
     }
     if (!sig.one()) settleScale(out, wp.opBegin, sig.re, sig.im);
-    // store layout: tile bits VB..VB+2 back on lane bits 0-2 (the vector bits
-    // never left their slots)
+    // store layout: the tile bits STORED to positions VB..VB+2 on lane bits
+    // 0-2 (one 128-byte line per 8 lanes; the vector bits never left their
+    // slots); with a relabelling pass these are other bits than at the load
+    int stBit[kWaveBits];
+    for (int b = 0; b < kWaveBits; b++) stBit[b] = -1;
+    for (int b = 0; b < kWaveBits; b++)
+        if (ps.stPos[b] < kWaveBits) stBit[ps.stPos[b]] = b;
     for (int l = 0; l < 3; l++) {
-        const int b = VB + l;
+        const int b = stBit[VB + l];
+        if (b < 0) return false;
         const int w = lay.where[b];
         if (w == kWaveSlots + l) continue;
         if (inSlot(w)) {
@@ -572,11 +616,12 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         }
     }
     // real lane bits 3.. may not carry positions above kWaveLanePosMax at store
+    auto farSt = [&](int b) { return ps.stPos[b] > kWaveLanePosMax; };
     for (int l = 3; l < kWaveLanes; l++) {
-        if (!farPos(lay.laneBit[l])) continue;
+        if (!farSt(lay.laneBit[l])) continue;
         int s = -1;
         for (int x = VB; x < kWaveSlots && s < 0; x++)
-            if (!farPos(lay.slotBit[x])) s = x;
+            if (!farSt(lay.slotBit[x])) s = x;
         if (s < 0) return false;  // cannot happen: at most kWaveSlots - 1 far bits
         transpose(s, l);
     }

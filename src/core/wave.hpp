@@ -115,6 +115,7 @@ struct WaveOp {
 
 struct WavePass {
     int pos[kWaveBits];        // tile bit -> physical position (pos[i] = i for i < 4)
+    int stPos[kWaveBits];      // tile bit -> physical position it is stored to (TilePass::stPos)
     int opBegin = 0, opEnd = 0;
     int ldSlot[kWaveSlots];    // tile bit held by slot s at load
     int ldLane[kWaveLaneBits]; // tile bit held by lane bit l at load (l >= 6: wave bits)
@@ -132,6 +133,15 @@ struct WaveProgram {
 // kWaveBits, non-contiguous low bits, Mat4 / DensChan2 ops, too many tile
 // bits above kWaveLanePosMax).
 bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out);
+
+// In-place relabelling passes (planTiles relabelFrom): on by default for
+// wave programs (QUEST_WAVE_RELABEL=0 / tuning "wave_relabel" turn it off).
+bool& waveRelabel();
+// Every relabelling pass of the program lowers to the wave engine (the LDS
+// and direct kernels store in place); false -> plan again without relabelling.
+bool relabelsLower(const TileProgram& prog);
+// After a program ran: the register's qubits moved by prog.perm.
+void applyProgramPerm(QuregImpl& q, const TileProgram& prog);
 
 // Cost in VALU instructions per lane of one transposition with lane bit l
 // (for the planner's statistics and tests).

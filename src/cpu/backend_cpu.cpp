@@ -505,19 +505,23 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
 long long g_trCost = 0;  // QUEST_WAVE_DUMP: weighted transposition cost (planner study)
 
 void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {
-    static thread_local i64 ld[kVLanes][kWaveRegs], st[kVLanes][kWaveRegs];
-    auto offsetOf = [&](const int* slotBit, const int* laneBit, int lane, int j) {
+    // shared by the threads of the parallel region below (a thread_local
+    // table here was filled by the calling thread only)
+    std::vector<i64> ldv((size_t)kVLanes * kWaveRegs), stv(ldv.size());
+    auto ld = reinterpret_cast<i64(*)[kWaveRegs]>(ldv.data());
+    auto st = reinterpret_cast<i64(*)[kWaveRegs]>(stv.data());
+    auto offsetOf = [&](const int* pos, const int* slotBit, const int* laneBit, int lane, int j) {
         i64 off = 0;
         for (int s = 0; s < kWaveSlots; s++)
-            if ((j >> s) & 1) off |= (i64)1 << ps.pos[slotBit[s]];
+            if ((j >> s) & 1) off |= (i64)1 << pos[slotBit[s]];
         for (int l = 0; l < kWaveLaneBits; l++)
-            if ((lane >> l) & 1) off |= (i64)1 << ps.pos[laneBit[l]];
+            if ((lane >> l) & 1) off |= (i64)1 << pos[laneBit[l]];
         return off;
     };
     for (int lane = 0; lane < kVLanes; lane++)
         for (int j = 0; j < kWaveRegs; j++) {
-            ld[lane][j] = offsetOf(ps.ldSlot, ps.ldLane, lane, j);
-            st[lane][j] = offsetOf(ps.stSlot, ps.stLane, lane, j);
+            ld[lane][j] = offsetOf(ps.pos, ps.ldSlot, ps.ldLane, lane, j);
+            st[lane][j] = offsetOf(ps.stPos, ps.stSlot, ps.stLane, lane, j);   // relabelling passes store permuted
         }
     static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;  // planner study: op mix per pass
     if (dump) {
@@ -637,8 +641,16 @@ void flush(QuregImpl& q) {
     }();
     const bool wave = planner == 3 && q.L >= kWaveBits;
     fuseBlockQubits() = wave ? 1 : 2;
-    static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : 5;  // as the HIP backend
-    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? waveCmin : 4, rt().fusion, prog);
+    static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : kWaveVecBits + 4;  // as the HIP backend
+    const bool relabel = wave && rt().fusion && waveRelabel() && !rt().verify;
+    std::vector<Op> orig;
+    if (relabel) orig = q.pending;
+    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? waveCmin : 4, rt().fusion, prog,
+              relabel ? kWaveVecBits : -1);
+    if (relabel && programRelabels(prog) && !relabelsLower(prog)) {
+        q.pending.swap(orig);
+        planTiles(q.pending, q.L, kWaveBits, waveCmin, rt().fusion, prog);
+    }
     if (trace::on())
         trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
                      q.pending.size(), prog.passes.size());
@@ -649,6 +661,7 @@ void flush(QuregImpl& q) {
     q.pending.clear();
     if (!rt().verify) {
         runProgram(q.re, q.im, q.L, prog, wave);
+        applyProgramPerm(q, prog);
         return;
     }
     // debug mode: the same ops one pass each, in order, on a shadow copy
