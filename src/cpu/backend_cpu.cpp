@@ -641,7 +641,7 @@ void flush(QuregImpl& q) {
     }();
     const bool wave = planner == 3 && q.L >= kWaveBits;
     fuseBlockQubits() = wave ? 1 : 2;
-    static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : kWaveVecBits + 4;  // as the HIP backend
+    static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : kWaveVecBits + 5;  // as the HIP backend
     const bool relabel = wave && rt().fusion && waveRelabel() && !rt().verify;
     std::vector<Op> orig;
     if (relabel) orig = q.pending;
