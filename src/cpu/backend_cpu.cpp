@@ -642,14 +642,17 @@ void flush(QuregImpl& q) {
     const bool wave = planner == 3 && q.L >= kWaveBits;
     fuseBlockQubits() = wave ? 1 : 2;
     static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : kWaveVecBits + 5;  // as the HIP backend
-    const bool relabel = wave && rt().fusion && waveRelabel() && !rt().verify;
+    bool channels = false;   // as the HIP backend: density-channel flushes keep one low position fewer
+    for (const Op& op : q.pending) channels = channels || op.kind == OpKind::Mat4 || op.kind == OpKind::DensChan2;
+    const int cminWave = channels ? kWaveVecBits + 4 : waveCmin;
+    const bool relabel = wave && !channels && rt().fusion && waveRelabel() && !rt().verify;
     std::vector<Op> orig;
     if (relabel) orig = q.pending;
-    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? waveCmin : 4, rt().fusion, prog,
+    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminWave : 4, rt().fusion, prog,
               relabel ? kWaveVecBits : -1);
     if (relabel && programRelabels(prog) && !relabelsLower(prog)) {
         q.pending.swap(orig);
-        planTiles(q.pending, q.L, kWaveBits, waveCmin, rt().fusion, prog);
+        planTiles(q.pending, q.L, kWaveBits, cminWave, rt().fusion, prog);
     }
     if (trace::on())
         trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
