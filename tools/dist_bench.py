@@ -1,0 +1,132 @@
+#!/usr/bin/env python3
+"""Distributed state-vector benchmark: R ranks x `qubits` local qubits, the
+random layered circuit of bench.py, with the exchange accounting the
+scaling analysis needs (swaps, bytes exchanged, time inside the all-to-all
+qubit swaps, from the library's trace events).
+
+One GPU (ranks share it through the device IPC transport, QUEST_COMM=ipc):
+
+    python tools/dist_bench.py --ranks 4 --qubits 30          # spawns the ranks
+
+Several GPUs (one rank per GPU over RCCL, started by torchrun):
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/dist_bench.py --worker --qubits 34
+
+The 37-qubit / 8 x MI355X configuration of BASELINE.json is `--qubits 34` on 8
+GPUs (256 GiB of state per GPU; getQuregMemoryPlan checks the budget first).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def worker(args):
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.models.circuits import Circuit
+
+    env = qa.Env()
+    rank, world = env.rank, env.num_ranks
+    n = args.qubits + int(round(math.log2(world)))
+    plan = qa.capi.getQuregMemoryPlan(n, world)   # dict: state, exchange, scratch, total
+    reg = qa.Register(env, n)
+    reg.init_plus()
+    layers = args.warmup + args.steps
+    circ = random_layered(n, layers, seed=7)
+    per = []
+    i = 0
+    for layer in range(layers):
+        cnt = n + len(range(layer % 2, n - 1, 2))
+        per.append(circ.gates[i:i + cnt])
+        i += cnt
+    for w in range(args.warmup):
+        Circuit(n, per[w]).apply(reg)
+    reg.sync()
+    qa.capi.resetQuESTStats()
+    env.sync()
+    t0 = time.perf_counter()
+    gates = 0
+    for s in range(args.steps):
+        Circuit(n, per[args.warmup + s]).apply(reg)
+        gates += len(per[args.warmup + s])
+    reg.sync()
+    env.sync()
+    dt = time.perf_counter() - t0
+    st = qa.capi.getQuESTStats()
+    norm = reg.total_prob()
+    swap_ms = []
+    tr = os.environ.get("QUEST_TRACE")
+    if tr and os.path.exists(tr):
+        for line in open(tr):
+            ev = json.loads(line)
+            if ev.get("ev") == "swap":
+                swap_ms.append(ev.get("host_ms", 0.0))
+    res = {"rank": rank, "ranks": world, "qubits": n, "local_qubits": args.qubits,
+           "transport": qa.capi.getQuESTTransport(), "s_per_gate": dt / max(gates, 1), "seconds": dt,
+           "gates": gates, "passes": st["passes"], "swaps": st["swaps"], "bytes_exchanged": st["bytesExchanged"],
+           "relabels": st["relabels"], "swap_host_ms": swap_ms, "norm_error": abs(norm - 1),
+           "memory_plan_bytes": plan}
+    out = args.out or os.environ.get("QUEST_DIST_BENCH_OUT")
+    if out:
+        with open(f"{out}.rank{rank}.json", "w") as f:
+            json.dump(res, f)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    reg.close()
+
+
+def launch(args):
+    with tempfile.TemporaryDirectory() as d:
+        env = {"QUEST_COMM": args.comm, "QUEST_DIST_BENCH_OUT": os.path.join(d, "res")}
+        # per-rank trace files for the swap timings
+        procs = []
+        script = [os.path.abspath(__file__), "--worker", "--qubits", str(args.qubits), "--steps", str(args.steps),
+                  "--warmup", str(args.warmup)]
+        import subprocess
+
+        from quest_amd.parallel import _free_port
+        port = _free_port()
+        for r in range(args.ranks):
+            e = dict(os.environ, RANK=str(r), WORLD_SIZE=str(args.ranks), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                     QUEST_BOOTSTRAP_ADDR="127.0.0.1", QUEST_BOOTSTRAP_PORT=str(port),
+                     QUEST_TRACE=os.path.join(d, f"trace{r}.jsonl"), **env)
+            procs.append(subprocess.Popen([sys.executable] + script, env=e, stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True))
+        outs = [p.communicate(timeout=args.timeout) for p in procs]
+        for r, (p, (so, se)) in enumerate(zip(procs, outs)):
+            if p.returncode != 0:
+                print(f"rank {r} failed ({p.returncode}):\n{se[-3000:]}", file=sys.stderr)
+                sys.exit(1)
+        ranks = [json.load(open(os.path.join(d, f"res.rank{r}.json"))) for r in range(args.ranks)]
+    worst = max(ranks, key=lambda x: x["seconds"])
+    summary = {"ranks": args.ranks, "qubits": worst["qubits"], "local_qubits": args.qubits,
+               "transport": ranks[0]["transport"], "s_per_gate": worst["s_per_gate"], "passes": ranks[0]["passes"],
+               "swaps": ranks[0]["swaps"], "bytes_exchanged_per_rank": ranks[0]["bytes_exchanged"],
+               "swap_host_ms_rank0": ranks[0]["swap_host_ms"], "norm_error": ranks[0]["norm_error"],
+               "memory_plan_bytes": ranks[0]["memory_plan_bytes"]}
+    print(json.dumps(summary))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--ranks", type=int, default=4)
+    ap.add_argument("--qubits", type=int, default=30, help="local qubits per rank")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--comm", default="ipc", help="QUEST_COMM for the spawned ranks (one GPU: ipc)")
+    ap.add_argument("--timeout", type=float, default=900)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    worker(args) if args.worker else launch(args)
+
+
+if __name__ == "__main__":
+    main()
