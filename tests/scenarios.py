@@ -231,6 +231,27 @@ def checkpoint_load(env):
 SCENARIOS.update({f.__name__: f for f in (checkpoint_save, checkpoint_load)})
 
 
+def layered_wave_relabel(env):
+    """16 qubits, 14 layers: with QUEST_CPU_PLANNER=3 every rank runs wave
+    passes that relabel its local qubits while the router swaps rank qubits
+    in and out (the two layout mechanisms together)."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    r = qa.Register(env, 16)
+    r.init_plus()
+    random_layered(16, 14, seed=21).apply(r)
+    probs = np.array([r.prob(q, 1) for q in range(16)])
+    amps = np.array([r.amp(i) for i in (0, 1, 12345, 65535)])
+    out = {"state": r.to_numpy(), "probs": probs, "amps": amps, "_swaps": capi.getQuESTStats()["swaps"]}
+    r.close()
+    return out
+
+
+SCENARIOS["layered_wave_relabel"] = layered_wave_relabel
+
+
 def hang_rank1(env):
     """Rank 1 stops responding; rank 0 must give up after QUEST_COMM_TIMEOUT."""
     import time

@@ -71,3 +71,17 @@ def test_sliced_pipelined_exchange(env, tmp_path, name):
     got = _multi(name, 4, tmp_path, QUEST_EXCHANGE_SLICE_KB="1")
     for k, v in want.items():
         np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_wave_relabelling_with_rank_swaps(env, tmp_path, ranks):
+    """Wave-planned ranks (host emulation, QUEST_CPU_PLANNER=3) whose passes
+    relabel local qubits, under the router's rank-qubit swaps: the same state
+    as one op-by-op process."""
+    want = _single("layered_wave_relabel", env)
+    got = _multi("layered_wave_relabel", ranks, tmp_path, QUEST_CPU_PLANNER="3")
+    for k, v in want.items():
+        if k.startswith("_"):
+            continue
+        np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+    assert int(got["_swaps"]) > 0
