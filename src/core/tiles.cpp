@@ -391,28 +391,41 @@ void remapOp(Op& op, const int* pi) {
     op.ctrl = c;
 }
 
-// Choose the store permutation of the pass just emitted (out.passes.back())
-// and apply it to the ops not yet scheduled.  The tile's positions >= from
-// hold some logical qubits; the ones the queue needs soonest (first op
-// targeting them) take the low positions [from, c), which every later tile
-// contains; the qubits they displace take the vacated high positions.
-void relabelPass(std::vector<Op>& ops, const std::vector<char>& done, int first, int from, int c, int L,
-                 TileProgram& out) {
-    TilePass& ps = out.passes.back();
+// Propose a store permutation for the pass just emitted (ps): the tile's
+// positions >= from hold some logical qubits; the ones the queue needs soonest
+// take the low positions [from, c), which every later tile contains, and the
+// qubits they displace take the vacated high positions.  `mode` ranks the
+// qubits: 0 by their first use in the queue, 1 by their uses among the next
+// 64 ops.  pi (a product of disjoint swaps, so its own inverse) is the
+// identity when nothing would move.
+bool proposePerm(const std::vector<Op>& ops, const std::vector<char>& done, int first, int from, int c,
+                 const TilePass& ps, int mode, int* pi) {
     const int INF = 1 << 30;
     int need[64];
-    for (int p = 0; p < 64; p++) need[p] = INF;
+    for (int p = 0; p < 64; p++) {
+        need[p] = INF;
+        pi[p] = p;
+    }
     u64 open = 0;
     for (int i = 0; i < ps.k; i++) open |= 1ull << ps.pos[i];
-    for (int i = first, rank = 0; i < (int)ops.size() && open; i++) {
-        if (done[i]) continue;
-        u64 tg = targetMask(ops[i]) & open;
-        for (; tg; tg &= tg - 1) {
-            const int p = __builtin_ctzll(tg);
-            need[p] = rank;
-            open &= ~(1ull << p);
+    if (mode == 1) {
+        int cnt[64] = {0};
+        for (int i = first, seen = 0; i < (int)ops.size() && seen < 64; i++) {
+            if (done[i]) continue;
+            seen++;
+            for (u64 tg = targetMask(ops[i]) & open; tg; tg &= tg - 1) cnt[__builtin_ctzll(tg)]++;
         }
-        rank++;
+        for (int p = 0; p < 64; p++) need[p] = cnt[p] ? 64 - cnt[p] : INF;
+    } else {
+        for (int i = first, rank = 0; i < (int)ops.size() && open; i++) {
+            if (done[i]) continue;
+            for (u64 tg = targetMask(ops[i]) & open; tg; tg &= tg - 1) {
+                const int p = __builtin_ctzll(tg);
+                need[p] = rank;
+                open &= ~(1ull << p);
+            }
+            rank++;
+        }
     }
     std::vector<int> cand;
     for (int i = 0; i < ps.k; i++)
@@ -436,8 +449,6 @@ void relabelPass(std::vector<Op>& ops, const std::vector<char>& done, int first,
         if (!chosenLow[p]) freeLow.push_back(p);
     // the low qubits needed latest make room first
     std::stable_sort(freeLow.begin(), freeLow.end(), [&](int a, int b) { return need[a] > need[b]; });
-    int pi[64];
-    for (int p = 0; p < 64; p++) pi[p] = p;
     bool any = false;
     for (size_t x = 0; x < in.size() && x < freeLow.size(); x++) {
         const int hi = in[x], lo = freeLow[x];
@@ -446,11 +457,12 @@ void relabelPass(std::vector<Op>& ops, const std::vector<char>& done, int first,
         pi[lo] = hi;
         any = true;
     }
-    if (!any) return;
-    for (int i = 0; i < ps.k; i++) ps.stPos[i] = pi[ps.pos[i]];
+    return any;
+}
+
+void applyPerm(std::vector<Op>& ops, const std::vector<char>& done, int first, const int* pi) {
     for (int i = first; i < (int)ops.size(); i++)
         if (!done[i]) remapOp(ops[i], pi);
-    for (int x = 0; x < L; x++) out.perm[x] = pi[out.perm[x]];
 }
 
 }  // namespace
@@ -571,8 +583,56 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             done[i] = 1;
         }
         emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out);
-        if (relabelFrom >= 0 && (int)best.size() >= 2 && (int)order.size() < n)
-            relabelPass(ops, done, first, relabelFrom, c, L, out);
+        if (relabelFrom >= 0 && (int)best.size() >= 2 && (int)order.size() < n) {
+            // candidate store permutations (none, by first use, by use count),
+            // each judged by how many ops the greedy plan of the NEXT pass
+            // then takes (QUEST_RELABEL_MODE=0/1 forces one candidate)
+            static const int forced = getenv("QUEST_RELABEL_MODE") ? atoi(getenv("QUEST_RELABEL_MODE")) : -1;
+            const TilePass ps = out.passes.back();
+            while (first < n && done[first]) first++;
+            auto nextPassOps = [&]() {
+                std::vector<int> pick;
+                size_t most = 0;
+                scan(0, pick);
+                most = pick.size();
+                int tries = 0;
+                for (int i = first; i < n && tries < 8; i++) {
+                    if (done[i]) continue;
+                    const u64 h = targetMask(ops[i]) & ~low;
+                    if (!h) continue;
+                    tries++;
+                    scan(h, pick);
+                    most = std::max(most, pick.size());
+                }
+                return most;
+            };
+            int pis[2][64];
+            bool has[2];
+            for (int m = 0; m < 2; m++) has[m] = proposePerm(ops, done, first, relabelFrom, c, ps, m, pis[m]);
+            int choice = -1;
+            if (forced >= 0) {
+                if (forced < 2 && has[forced]) choice = forced;
+            } else {
+                size_t bestNext = nextPassOps();
+                for (int m = 0; m < 2; m++) {
+                    if (!has[m] || (m == 1 && has[0] && !memcmp(pis[0], pis[1], sizeof pis[0]))) continue;
+                    applyPerm(ops, done, first, pis[m]);
+                    const size_t v = nextPassOps();
+                    applyPerm(ops, done, first, pis[m]);   // involution: undo
+                    if (v > bestNext || (v == bestNext && choice < 0 && m == 0)) {
+                        bestNext = v;
+                        choice = m;
+                    }
+                }
+            }
+            if (choice >= 0) {
+                const int* pi = pis[choice];
+                TilePass& last = out.passes.back();
+                for (int i = 0; i < last.k; i++) last.stPos[i] = pi[last.pos[i]];
+                applyPerm(ops, done, first, pi);
+                for (int x = 0; x < L; x++) out.perm[x] = pi[out.perm[x]];
+            }
+        }
     }
     ops.swap(order);
 }

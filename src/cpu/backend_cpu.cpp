@@ -619,14 +619,22 @@ void freeState(QuregImpl& q) {
 void* allocComm(size_t bytes) { return malloc(bytes ? bytes : 1); }
 void freeComm(void* p) { free(p); }
 
+// ops queued before a flush: the HIP backend's 1024 (QUEST_QUEUE_OPS), so
+// that the emulated wave plans are the GPU's
 void enqueue(QuregImpl& q, const Op& op) {
+    static const size_t limit = [] {
+        const char* e = getenv("QUEST_QUEUE_OPS");
+        const long v = e ? atol(e) : 1024;
+        return (size_t)std::max(1L, std::min(v, 1024L));
+    }();
     q.pending.push_back(op);
-    if (q.pending.size() >= 512) flush(q);
+    if (q.pending.size() >= limit) flush(q);
 }
 
 void flush(QuregImpl& q) {
     if (q.pending.empty()) return;
     stats().flushes++;
+    const double tFlush0 = trace::on() ? trace::now() : 0.0;
     const size_t opsIn = q.pending.size();
     TileProgram prog;
     std::vector<Op> raw;
@@ -655,13 +663,25 @@ void flush(QuregImpl& q) {
         planTiles(q.pending, q.L, kWaveBits, cminWave, rt().fusion, prog);
     }
     if (trace::on())
-        trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu", q.L, opsIn,
-                     q.pending.size(), prog.passes.size());
+        trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu, \"plan_ms\": %.3f",
+                     q.L, opsIn, q.pending.size(), prog.passes.size(), 1e3 * (trace::now() - tFlush0));
     if (planner == 1)
         planPhases(prog, -1, regSlots());
     else if (planner == 2)
         planDenseBlocks(prog, -1, regSlots());
     q.pending.clear();
+    // QUEST_PLAN_ONLY=1 (planner studies): plan, count, do not touch the
+    // state -- pass counts of large registers in no time (tools/plan_study.py)
+    static const bool planOnly = getenv("QUEST_PLAN_ONLY") && atoi(getenv("QUEST_PLAN_ONLY")) != 0;
+    if (planOnly) {
+        for (const TilePass& ps : prog.passes) {
+            WaveProgram wp;
+            if (wave && planWavePass(ps, prog.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, wp)) stats().wavePasses++;
+            stats().passes++;
+        }
+        applyProgramPerm(q, prog);
+        return;
+    }
     if (!rt().verify) {
         runProgram(q.re, q.im, q.L, prog, wave);
         applyProgramPerm(q, prog);
