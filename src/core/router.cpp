@@ -789,7 +789,12 @@ double probZero(QuregImpl& q, int qubit) {
     drain(q);
     if (marginalCacheOn() && q.margGen == q.stateGen) return q.margP0[qubit];
     stats().reductions++;
-    if (marginalCacheOn() && q.probGen == q.stateGen) {
+    // a qubit on one of the lowest local positions shares every 128-byte
+    // line between its two halves: its own reduction streams the whole
+    // chunk anyway, so compute every marginal in that pass
+    const int pq = q.l2p[qubit];
+    const bool wholeLines = pq < q.L && ((i64)sizeof(real) << pq) < 128;
+    if (marginalCacheOn() && (q.probGen == q.stateGen || wholeLines)) {
         double z[65], tot;
         be::marginals(q, z, &tot);
         double v[65];
