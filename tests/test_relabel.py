@@ -95,3 +95,45 @@ def test_relabelling_cuts_passes():
         assert out.returncode == 0, out.stderr[-2000:]
         res[relabel] = int(out.stdout.split()[-1])
     assert res["1"] < res["0"], res
+
+
+DENSITY = r'''
+import os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import quest_amd as qa
+from helpers import apply_random_ops, oracle_for
+from quest_amd.ops import capi
+
+env = qa.Env()
+n = 7                      # 14 state-vector qubits: wave passes on the host emulation
+r = qa.Register(env, n, density=True)
+rng = np.random.default_rng(5)
+o = oracle_for(r, rng)
+apply_random_ops(r, o, rng, 120)          # gates only: the flushes relabel
+r.flush()
+moved = sum(1 for lg, p in enumerate(capi.getQubitLayout(r.q)) if lg != p)
+print("moved", moved)
+assert moved > 0
+assert np.max(np.abs(r.to_numpy() - o.rho)) < 1e-11
+assert abs(r.purity() - o.purity()) < 1e-11
+assert abs(r.total_prob() - np.real(np.trace(o.rho))) < 1e-11
+for q in range(n):
+    assert abs(r.prob(q, 0) - o.prob(q, 0)) < 1e-11
+for (i, j) in [(0, 0), (3, 5), (127, 64)]:
+    a = capi.getDensityAmp(r.q, i, j)
+    assert abs(complex(a.real, a.imag) - o.rho[i, j]) < 1e-11
+psi = qa.Register(env, n)
+psi.init_plus()
+f = capi.calcFidelity(r.q, psi.q)
+v = np.full(1 << n, 1 / np.sqrt(1 << n))
+assert abs(f - np.real(np.conj(v) @ o.rho @ v)) < 1e-11
+print("density relabel ok")
+'''
+
+
+def test_relabelled_density_matrix_reads():
+    out = subprocess.run([sys.executable, "-c", DENSITY, ROOT], cwd=ROOT, capture_output=True, text=True,
+                         timeout=600, env=dict(os.environ, QUEST_BACKEND="cpu", QUEST_CPU_PLANNER="3"))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "density relabel ok" in out.stdout
