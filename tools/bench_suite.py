@@ -179,10 +179,20 @@ def run_density17(env, res, n=17):
     t_gate = (time.perf_counter() - t0) / ng
     tr = d.total_prob()
     pur = d.purity()
+    # a deeper random layered circuit (the q34 workload) on the density
+    # matrix: each gate is U on the row qubit and conj(U) on the column qubit
+    from quest_amd.models import random_layered
+
+    c = random_layered(n, 6, seed=17)
+    d.sync()
+    t0 = time.perf_counter()
+    c.apply(d)
+    d.sync()
+    t_layered = (time.perf_counter() - t0) / len(c.gates)
     res["density17"] = {"qubits": n, "amps": 1 << (2 * n), "damping_s_per_channel": t_damp,
-                        "gate_s": t_gate, "trace": tr, "purity": pur}
-    print(f"density{n}: damping {1e3 * t_damp:.2f} ms/channel, gates {1e3 * t_gate:.2f} ms/gate, "
-          f"trace {tr:.12f}, purity {pur:.6f}", flush=True)
+                        "gate_s": t_gate, "layered_s_per_gate": t_layered, "trace": tr, "purity": pur}
+    print(f"density{n}: damping {1e3 * t_damp:.2f} ms/channel, gates {1e3 * t_gate:.2f} ms/gate (one layer), "
+          f"layered {1e3 * t_layered:.2f} ms/gate (6 layers), trace {tr:.12f}, purity {pur:.6f}", flush=True)
     d.close()
 
 
