@@ -151,7 +151,9 @@ def main():
             "global_batch": 1,
             "seq_len": 1 << n,
             "gates_per_step": gates / max(args.steps, 1),
-            "parallelism": f"dp{world}: amplitude-sharded over {world} GPU(s), qubit swaps over RCCL",
+            "parallelism": f"dp{world}: amplitude-sharded over {world} GPU(s)" +
+                           ("" if world == 1 else ", all-to-all qubit swaps over " +
+                            ("RCCL" if transport.startswith("RCCL") else transport)),
             "transport": transport,
             "fusion": not args.eager,
             "passes": stats["passes"],
