@@ -61,6 +61,19 @@ def worker(args):
     dt = time.perf_counter() - t0
     st = qa.capi.getQuESTStats()
     norm = reg.total_prob()
+    # latency of a distributed scalar read (local reduction + allreduce of
+    # one fp64 through the transport) and of an amplitude read (owner read +
+    # broadcast), the reference's MPI_Allreduce / MPI_Bcast call sites
+    reps = 20
+    env.sync()
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        reg.total_prob()
+    scalar_ms = 1e3 * (time.perf_counter() - t1) / reps
+    t1 = time.perf_counter()
+    for i in range(reps):
+        reg.amp((i * 7919) % (1 << n))
+    amp_ms = 1e3 * (time.perf_counter() - t1) / reps
     swap_ms = []
     tr = os.environ.get("QUEST_TRACE")
     if tr and os.path.exists(tr):
@@ -72,6 +85,7 @@ def worker(args):
            "transport": qa.capi.getQuESTTransport(), "s_per_gate": dt / max(gates, 1), "seconds": dt,
            "gates": gates, "passes": st["passes"], "swaps": st["swaps"], "bytes_exchanged": st["bytesExchanged"],
            "relabels": st["relabels"], "swap_host_ms": swap_ms, "norm_error": abs(norm - 1),
+           "total_prob_ms": scalar_ms, "get_amp_ms": amp_ms,
            "memory_plan_bytes": plan}
     out = args.out or os.environ.get("QUEST_DIST_BENCH_OUT")
     if out:
@@ -110,6 +124,7 @@ def launch(args):
                "transport": ranks[0]["transport"], "s_per_gate": worst["s_per_gate"], "passes": ranks[0]["passes"],
                "swaps": ranks[0]["swaps"], "bytes_exchanged_per_rank": ranks[0]["bytes_exchanged"],
                "swap_host_ms_rank0": ranks[0]["swap_host_ms"], "norm_error": ranks[0]["norm_error"],
+               "total_prob_ms": ranks[0]["total_prob_ms"], "get_amp_ms": ranks[0]["get_amp_ms"],
                "memory_plan_bytes": ranks[0]["memory_plan_bytes"]}
     print(json.dumps(summary))
 
