@@ -443,8 +443,13 @@ def test_checkpoint_round_trip_gpu(genv, tmp_path):
     assert r.save(tmp_path / "ck")
     s = qa.Register(genv, 24)
     assert s.load(tmp_path / "ck")
-    assert [s.prob(q, 1) for q in (0, 11, 23)] == want_p
+    # the amplitudes come back bit for bit; the marginals only to rounding,
+    # since the source register may sit in a relabelled qubit layout (its
+    # sums run over the amplitudes in another order) and the loaded one in
+    # the identity layout
+    np.testing.assert_allclose([s.prob(q, 1) for q in (0, 11, 23)], want_p, rtol=0, atol=1e-14)
     assert s.amp(12345) == amp
+    np.testing.assert_array_equal(s.to_numpy(), r.to_numpy())
     assert abs(s.inner(r) - 1) < 1e-12
     r.close()
     s.close()
