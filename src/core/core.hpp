@@ -87,6 +87,8 @@ struct QuregImpl {
     u64 margGen = ~0ull;
     u64 probGen = ~0ull;      // state generation of the last single-qubit query
     double margP0[65];
+    u64 normGen = ~0ull;      // state generation of normCache (sumSqAll)
+    double normCache = 0;
     real* hostRe = nullptr;   // optional host mirror (Qureg.stateVec)
     real* hostIm = nullptr;
     bool permIdentity() const {

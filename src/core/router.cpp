@@ -819,10 +819,16 @@ double probZero(QuregImpl& q, int qubit) {
     return allSum(part);
 }
 
+// The norm, cached like the marginals: a normalisation check after every
+// measurement round or a repeated calcTotalProb reads the state once.
 double sumSqAll(QuregImpl& q) {
     drain(q);
+    if (marginalCacheOn() && q.margGen == q.stateGen) return q.margP0[q.nSV];
+    if (marginalCacheOn() && q.normGen == q.stateGen) return q.normCache;
     stats().reductions++;
-    return allSum(be::sumSq(q, -1, 0));
+    q.normCache = allSum(be::sumSq(q, -1, 0));
+    q.normGen = q.stateGen;
+    return q.normCache;
 }
 
 static double densDiag(QuregImpl& q, int skipBit) {

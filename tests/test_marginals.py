@@ -52,6 +52,7 @@ def test_cache_invalidated_by_every_state_change(env, rng):
     def check():
         for q in (0, 7, n - 1):
             assert r.prob(q, 0) == pytest.approx(_marg(o.v, n, q)[0], abs=1e-12)
+        assert r.total_prob() == pytest.approx(np.vdot(o.v, o.v).real, abs=1e-12)
 
     check()
     r.h(3)
@@ -74,7 +75,7 @@ def test_cache_invalidated_by_every_state_change(env, rng):
     # host buffers -> state
     import torch
 
-    v = np.roll(o2.v, 3)
+    v = 1.5 * np.roll(o2.v, 3)     # unnormalised: the cached norm must change
     r.from_torch(torch.from_numpy(v))
     o.v = v
     check()
@@ -107,4 +108,23 @@ def test_density_probabilities_unaffected(env, rng):
         d = np.real(np.diag(o.rho)).reshape([2] * 4)
         axes = tuple(3 - k for k in range(4) if k != q)
         assert r.prob(q, 0) == pytest.approx(d.sum(axis=axes)[0], abs=1e-12)
+    r.close()
+
+
+def test_norm_cached_per_state(env, rng):
+    """calcTotalProb reads the state once per state change (router::sumSqAll)."""
+    import quest_amd as qa
+
+    r = qa.Register(env, 12)
+    o = oracle_for(r, rng)
+    apply_random_ops(r, o, rng, 30)
+    r.sync()
+    before = capi.getQuESTStats()["reductions"]
+    for _ in range(5):
+        assert r.total_prob() == pytest.approx(1.0, abs=1e-12)
+    assert capi.getQuESTStats()["reductions"] - before == 1
+    r.x(2)
+    o.apply(O.X, 2)
+    r.total_prob()
+    assert capi.getQuESTStats()["reductions"] - before == 2
     r.close()
