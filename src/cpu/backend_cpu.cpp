@@ -504,6 +504,26 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
 
 long long g_trCost = 0;  // QUEST_WAVE_DUMP: weighted transposition cost (planner study)
 
+// QUEST_WAVE_DUMP (planner study): the op mix of every wave pass on stderr
+static void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
+    static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;
+    if (!dump) return;
+    int cnt[32] = {0}, trw = 0, ctl = 0;
+    for (int i = ps.opBegin; i < ps.opEnd; i++) {
+        const WaveOp& w = wp.ops[(size_t)i];
+        cnt[w.kind]++;
+        if (w.kind == (int)WKind::TR && w.b >= kWaveLanes) trw++;
+        if (w.kind == (int)WKind::TR) g_trCost += waveTransposeCost(w.b);
+        if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
+    }
+    fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d "
+            "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d chan %d\n",
+            ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
+            cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
+            cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24]);
+    fprintf(stderr, "wave: cumulative weighted transposition cost %lld\n", g_trCost);
+}
+
 void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {
     // shared by the threads of the parallel region below (a thread_local
     // table here was filled by the calling thread only)
@@ -523,23 +543,7 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
             ld[lane][j] = offsetOf(ps.pos, ps.ldSlot, ps.ldLane, lane, j);
             st[lane][j] = offsetOf(ps.stPos, ps.stSlot, ps.stLane, lane, j);   // relabelling passes store permuted
         }
-    static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;  // planner study: op mix per pass
-    if (dump) {
-        int cnt[32] = {0}, trw = 0, ctl = 0;
-        for (int i = ps.opBegin; i < ps.opEnd; i++) {
-            const WaveOp& w = wp.ops[(size_t)i];
-            cnt[w.kind]++;
-            if (w.kind == (int)WKind::TR && w.b >= kWaveLanes) trw++;
-            if (w.kind == (int)WKind::TR) g_trCost += waveTransposeCost(w.b);
-            if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
-        }
-        fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d "
-                "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d chan %d\n",
-                ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
-                cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
-                cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24]);
-        fprintf(stderr, "wave: cumulative weighted transposition cost %lld\n", g_trCost);
-    }
+    dumpWavePass(wp, ps);
     TilePass tp;
     tp.k = kWaveBits;
     for (int b = 0; b < kWaveBits; b++) tp.pos[b] = ps.pos[b];
@@ -676,7 +680,10 @@ void flush(QuregImpl& q) {
     if (planOnly) {
         for (const TilePass& ps : prog.passes) {
             WaveProgram wp;
-            if (wave && planWavePass(ps, prog.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, wp)) stats().wavePasses++;
+            if (wave && planWavePass(ps, prog.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, wp)) {
+                stats().wavePasses++;
+                dumpWavePass(wp, wp.passes.back());
+            }
             stats().passes++;
         }
         applyProgramPerm(q, prog);

@@ -70,6 +70,12 @@ CH_KINDS = ["CH1", "CHD"]
 LAYOUT = {}
 
 
+# op record fields live in s[36:59] (prefetch buffer) and s[68:91] (the
+# running handler's copy): handler, cReg, cLane, aux, ctrlOut (2), cWave,
+# cWaveZero, m[8] (fp64) / m[16] (fp32)
+REC_LO, REC_HI = 68, 91
+
+
 def set_layout(R):
     """Base index of every handler family for R register slots; the last
     entry ("done") is the end-of-list sentinel (the store epilogue)."""
@@ -223,7 +229,9 @@ def schedule(body):
 
 
 class Gen:
-    def __init__(self, R, dbuf, W, P=2, debug=False):
+    def __init__(self, R, dbuf, W, P=2, debug=False, stagger=0, nomem=False):
+        self.stagger = stagger
+        self.nomem = nomem      # experiment: no state loads / stores (compute time alone)
         self.debug = debug
         self.R = R
         self.NS = 1 << R
@@ -249,6 +257,7 @@ class Gen:
         self.CL = D + 18 * P + 4       # 4 values: per-lane coefficients of the lane-bit gates
         self.nvgpr = D + 22 * P + 4    # fp64 R = 4: 112 VGPRs, 4 waves per SIMD
         self.handlers = {}
+        self.hstart = None       # first body line of the handler being generated
         self.buf = None          # straight-line region being collected for scheduling
 
     # ---- helpers --------------------------------------------------------
@@ -290,58 +299,94 @@ class Gen:
         return r + self.P - 1
 
     def handler(self, idx, name):
+        self.finish_handler()
         lab = f"wh_{name}"
         self.handlers[idx] = lab
         self.lines.append("")
         self.lines.append(f"\t.p2align 2")
         self.label(lab)
+        self.hstart = len(self.lines)
+
+    def finish_handler(self):
+        """Prologue of the handler just generated: copy the fields of its op
+        record that its body reads (s68..s91) out of the prefetch buffer
+        s[36:59], then prefetch the next record into the buffer.  A handler
+        copies only what it uses (a CNOT its two control words, a rotation
+        two coefficients) instead of every handler copying all 24 dwords."""
+        if self.hstart is None:
+            return
+        used = set()
+        for ln in self.lines[self.hstart:]:
+            for a, b in re.findall(r"s\[(\d+):(\d+)\]", ln):
+                used.update(range(int(a), int(b) + 1))
+            for a in re.findall(r"\bs(\d+)\b", ln):
+                used.add(int(a))
+        used = sorted(d for d in used if REC_LO <= d <= REC_HI)
+        pro = []
+        k = 0
+        while k < len(used):
+            d = used[k]
+            if d % 2 == 0 and k + 1 < len(used) and used[k + 1] == d + 1:
+                pro.append(f"\ts_mov_b64 s[{d}:{d + 1}], s[{d - 32}:{d - 31}]")
+                k += 2
+            else:
+                pro.append(f"\ts_mov_b32 s{d}, s{d - 32}")
+                k += 1
+        pro += ["\ts_add_u32 s94, s94, 96",
+                "\ts_addc_u32 s95, s95, 0",
+                "\ts_load_dwordx8 s[36:43], s[94:95], 0x0",
+                "\ts_load_dwordx16 s[44:59], s[94:95], 0x20"]
+        self.lines[self.hstart:self.hstart] = pro
+        self.hstart = None
 
     def back(self):
         self.next_op()
 
     def next_op(self):
         """Start the next op (inlined at the end of every handler: one taken
-        branch per op).  Op k+1's record was prefetched into s[36:59] while op
-        k ran; it is moved to s[68:91] and op k+2 is prefetched.  The list
-        ends with a sentinel record whose handler is the store epilogue; ops
-        that need tile / wave predicates have bit 31 of the handler offset set
-        and take the shared check path (rare)."""
+        branch per op).  Op k+1's record was prefetched into s[36:59] by op
+        k's prologue; op k+1's own prologue copies the fields it reads to
+        s[68:91] and prefetches op k+2 (finish_handler).  The list ends with a
+        sentinel record whose handler is the store epilogue; ops that need
+        tile / wave predicates have bit 31 of the handler offset set and take
+        the shared check path (rare)."""
         e = self.e
         e("s_waitcnt lgkmcnt(0)")
-        for k in range(0, 24, 2):
-            e(f"s_mov_b64 s[{68 + k}:{69 + k}], s[{36 + k}:{37 + k}]")
-        e("s_add_u32 s94, s94, 96")
-        e("s_addc_u32 s95, s95, 0")
-        e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
-        e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
         # flagged ops (bit 31) go to the shared check path: selected as the
         # jump target rather than branched to (handlers lie > 128 KiB away)
-        e("s_bitcmp1_b32 s68, 31")
-        e("s_cselect_b32 s98, .Lcheck-qa_wave_tile, s68")
+        e("s_bitcmp1_b32 s36, 31")
+        e("s_cselect_b32 s98, .Lcheck-qa_wave_tile, s36")
         e("s_add_u32 s98, s92, s98")                   # kernel base + handler offset
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
 
     def check_path(self):
-        """Shared slow path of next_op: skip the op (start the next one) unless
-        the tile satisfies its out-of-tile controls and this wave its
-        wave-bit controls, else dispatch it."""
+        """Shared slow path of next_op: skip the op (prefetch the one after
+        it and start that) unless the tile satisfies its out-of-tile controls
+        and this wave its wave-bit controls, else dispatch it.  The record is
+        still in the prefetch buffer s[36:59]."""
         e = self.e
         self.label(".Lcheck")
-        e("s_and_b64 s[96:97], s[32:33], s[72:73]")    # ctrlOut of the op
-        e("s_cmp_eq_u64 s[96:97], s[72:73]")
-        e("s_cbranch_scc0 .Lnext")
+        e("s_and_b64 s[96:97], s[32:33], s[40:41]")    # ctrlOut of the op
+        e("s_cmp_eq_u64 s[96:97], s[40:41]")
+        e("s_cbranch_scc0 .Lskip_op")
         if self.W:
-            e("s_and_b32 s96, s3, s74")                 # wave bits that must be 1
-            e("s_cmp_eq_u32 s96, s74")
-            e("s_cbranch_scc0 .Lnext")
-            e("s_and_b32 s96, s3, s75")                 # wave bits that must be 0
+            e("s_and_b32 s96, s3, s42")                 # wave bits that must be 1
+            e("s_cmp_eq_u32 s96, s42")
+            e("s_cbranch_scc0 .Lskip_op")
+            e("s_and_b32 s96, s3, s43")                 # wave bits that must be 0
             e("s_cmp_eq_u32 s96, 0")
-            e("s_cbranch_scc0 .Lnext")
-        e("s_bitset0_b32 s68, 31")
-        e("s_add_u32 s98, s92, s68")
+            e("s_cbranch_scc0 .Lskip_op")
+        e("s_bitset0_b32 s36, 31")
+        e("s_add_u32 s98, s92, s36")
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
+        self.label(".Lskip_op")
+        e("s_add_u32 s94, s94, 96")
+        e("s_addc_u32 s95, s95, 0")
+        e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
+        e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
+        e("s_branch .Lnext")
 
     # ---- predication: per register j, exec = lanes whose controls hold ----
     def ctrl_begin(self):
@@ -934,6 +979,22 @@ class Gen:
         e("s_lshl_b32 s16, s16, s95")                # (w % 8) C P
         e("s_add_u32 s16, s16, s98")
         self.label(".Lmap_done")
+        if self.stagger:
+            # experiment: the odd workgroup of a CU starts `stagger` x 8128
+            # cycles late, so the two resident tiles of a CU run out of phase
+            # (one loading or storing while the other computes)
+            e("s_bfe_u32 s97, s99, 0x80000")
+            e("s_lshr_b32 s98, s2, 3")
+            e("s_lshr_b32 s98, s98, s97")
+            e("s_bitcmp1_b32 s98, 0")
+            e("s_cbranch_scc0 .Lstagger_done")
+            e(f"s_mov_b32 s98, {self.stagger}")
+            self.label(".Lstagger")
+            e("s_sleep 127")
+            e("s_sub_u32 s98, s98, 1")
+            e("s_cmp_lg_u32 s98, 0")
+            e("s_cbranch_scc1 .Lstagger")
+            self.label(".Lstagger_done")
         e("s_mov_b32 s17, 0")
         e("s_waitcnt vmcnt(0) lgkmcnt(0)")
         if self.dbuf:
@@ -1049,6 +1110,7 @@ class Gen:
             for creg in range(NS):
                 for lane in (0, 1):
                     self.gen_ph(kind, creg, lane)
+        self.finish_handler()
         L.append(".Lfunc_end0:")
         L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
         self.descriptor()
@@ -1119,6 +1181,8 @@ class Gen:
                 e(f"s_addc_u32 s{Q + 1}, s{arr + 1}, s{bpair + 1}")
                 e(f"s_add_u32 s{Q}, s{Q}, s{g}")
                 e(f"s_addc_u32 s{Q + 1}, s{Q + 1}, s{g + 1}")
+                if self.nomem:
+                    continue
                 if what == "ld":
                     e(f"buffer_load_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen{LD_POLICY}")
                 else:
@@ -1224,6 +1288,8 @@ def main():
     ap.add_argument("--dbuf", type=int, default=-1, help="software-pipelined tiles (default: when 4 slots)")
     ap.add_argument("--wbits", type=int, default=3, help="2^wbits waves share a tile")
     ap.add_argument("--debug", action="store_true", help="record addressing state per wave and stop (no state access)")
+    ap.add_argument("--stagger", type=int, default=0, help="start odd workgroups of a CU N x 8128 cycles late")
+    ap.add_argument("--nomem", action="store_true", help="experiment: drop the state loads and stores")
     ap.add_argument("--out", required=True)
     ap.add_argument("--obj")
     ap.add_argument("--hsaco")
@@ -1233,7 +1299,7 @@ def main():
         # a tile has <= 4 waves (otherwise too few workgroups fit a CU)
         dbuf = args.dbuf if args.dbuf >= 0 else (args.slots <= 4 and args.wbits <= 2)
         set_layout(args.slots)
-        g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug)
+        g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug, args.stagger, args.nomem)
         g.kernel()
         with open(args.out, "w") as f:
             f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
