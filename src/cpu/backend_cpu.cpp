@@ -521,7 +521,12 @@ static void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
             ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
             cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
             cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24]);
-    fprintf(stderr, "wave: cumulative weighted transposition cost %lld\n", g_trCost);
+    int trb[16] = {0};
+    for (int i = ps.opBegin; i < ps.opEnd; i++)
+        if (wp.ops[(size_t)i].kind == (int)WKind::TR) trb[wp.ops[(size_t)i].b & 15]++;
+    fprintf(stderr, "wave: TR per bit:");
+    for (int b = 0; b < 9; b++) fprintf(stderr, " %d", trb[b]);
+    fprintf(stderr, "\nwave: cumulative weighted transposition cost %lld\n", g_trCost);
 }
 
 void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {

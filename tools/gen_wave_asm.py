@@ -82,7 +82,9 @@ def set_layout(R):
     NS = 1 << R
     sizes = [("slot", len(KINDS) * 2 * R), ("d2s", 2 * R), ("d2l", 2), ("tr", 6 * R), ("diag", 2 * NS),
              ("trw", 4 * R), ("lane", 8 * len(LANE_KINDS)), ("slot2", len(KINDS2) * 2 * R),
-             ("ph", len(PH_KINDS) * 2 * NS), ("ch", len(CH_KINDS) * R * R)]
+             ("ph", len(PH_KINDS) * 2 * NS), ("ch", len(CH_KINDS) * R * R),
+             # controls on lane bits only (cReg 0): exec set once, no per-register tests
+             ("slotL", len(KINDS) * R), ("slot2L", len(KINDS2) * R), ("d2sL", R)]
     LAYOUT.clear()
     LAYOUT["R"] = R
     i = 0
@@ -93,10 +95,14 @@ def set_layout(R):
 
 
 def idx_slot(kind, s, ctrl):
+    if ctrl == 2:
+        return LAYOUT["slotL"] + KINDS.index(kind) * LAYOUT["R"] + s
     return LAYOUT["slot"] + KINDS.index(kind) * 2 * LAYOUT["R"] + s * 2 + ctrl
 
 
 def idx_d2s(s, ctrl):
+    if ctrl == 2:
+        return LAYOUT["d2sL"] + s
     return LAYOUT["d2s"] + s * 2 + ctrl
 
 
@@ -121,6 +127,8 @@ def idx_lane(kind, l, ctrl):
 
 
 def idx_slot2(kind, s, ctrl):
+    if ctrl == 2:
+        return LAYOUT["slot2L"] + KINDS2.index(kind) * LAYOUT["R"] + s
     return LAYOUT["slot2"] + KINDS2.index(kind) * 2 * LAYOUT["R"] + s * 2 + ctrl
 
 
@@ -258,6 +266,7 @@ class Gen:
         self.nvgpr = D + 22 * P + 4    # fp64 R = 4: 112 VGPRs, 4 waves per SIMD
         self.handlers = {}
         self.hstart = None       # first body line of the handler being generated
+        self.lane_ctrl = False   # generating a ctrl-2 (lane controls only) handler
         self.buf = None          # straight-line region being collected for scheduling
 
     # ---- helpers --------------------------------------------------------
@@ -517,8 +526,18 @@ class Gen:
         self.e(f"{self.op('fma')} {y}, {self.vp(cr)}, {y}, {T[1]}")
 
     # ---- handlers --------------------------------------------------------
+    def lane_exec_begin(self):
+        """ctrl 2 (controls on lane bits only): exec = the lanes whose cLane
+        bits are set, once for the whole handler."""
+        self.ctrl_begin()
+        self.e("s_mov_b64 exec, s[96:97]")
+
     def gen_slot(self, kind, s, ctrl):
         self.handler(idx_slot(kind, s, ctrl), f"{kind}_s{s}_c{ctrl}")
+        if ctrl == 2:
+            self.lane_exec_begin()
+            ctrl = 0
+            self.lane_ctrl = True
         if ctrl:
             self.ctrl_begin()
         else:
@@ -536,10 +555,20 @@ class Gen:
             self.ctrl_end()
         else:
             self.end_region()
+        self.lane_ctrl_end()
         self.back()
+
+    def lane_ctrl_end(self):
+        if self.lane_ctrl:
+            self.ctrl_end()
+            self.lane_ctrl = False
 
     def gen_slot2(self, kind, s, ctrl):
         self.handler(idx_slot2(kind, s, ctrl), f"{kind}_s{s}_c{ctrl}")
+        if ctrl == 2:
+            self.lane_exec_begin()
+            ctrl = 0
+            self.lane_ctrl = True
         if ctrl:
             self.ctrl_begin()
         else:
@@ -557,6 +586,7 @@ class Gen:
             self.ctrl_end()
         else:
             self.end_region()
+        self.lane_ctrl_end()
         self.back()
 
     def gen_ph(self, kind, creg, lane):
@@ -612,6 +642,10 @@ class Gen:
 
     def gen_d2s(self, s, ctrl):
         self.handler(idx_d2s(s, ctrl), f"D2S_s{s}_c{ctrl}")
+        if ctrl == 2:
+            self.lane_exec_begin()
+            ctrl = 0
+            self.lane_ctrl = True
         if ctrl:
             self.ctrl_begin()
         else:
@@ -629,6 +663,7 @@ class Gen:
             self.ctrl_end()
         else:
             self.end_region()
+        self.lane_ctrl_end()
         self.back()
 
     def gen_d2l(self, ctrl):
@@ -881,8 +916,12 @@ class Gen:
         self.handler(idx_trw(s, b), f"TRW_s{s}_b{b}")
         e = self.e
         vt, vl = self.vTmp, self.vLane
+        # registers j .. j + chunk - 1 with the same slot bit s are adjacent
+        # VGPRs: move them with one LDS instruction of up to 16 bytes
+        chunk = min(1 << s, 4 // self.P)
+        width = chunk * self.P            # dwords per LDS instruction
         lo_regs, hi_regs = [], []
-        for j in range(self.NS):
+        for j in range(0, self.NS, chunk):
             if (j >> s) & 1:
                 continue
             f = j | (1 << s)
@@ -890,7 +929,7 @@ class Gen:
             hi_regs += [self.re(j), self.im(j)]
         ob = self.OUTBOX
         e(f"s_mul_i32 s96, s3, {ob}")
-        e(f"v_lshlrev_b32_e32 v{vt}, {2 if self.P == 1 else 3}, v{vl}")
+        e(f"v_lshlrev_b32_e32 v{vt}, {(4 * width).bit_length() - 1}, v{vl}")
         e(f"v_add_u32_e32 v{vt}, s96, v{vt}")
         for phase in ("w", "r"):
             e(f"s_bitcmp1_b32 s3, {b}")
@@ -899,11 +938,12 @@ class Gen:
                 if tag == "hi":
                     self.label(f".Ltrw_{s}_{b}_{phase}hi")
                 for k, r in enumerate(regs):
-                    stride = 256 * self.P
+                    stride = 64 * 4 * width
+                    vr = f"v[{r}:{r + width - 1}]" if width > 1 else f"v{r}"
                     if phase == "w":
-                        e(f"ds_write_b{32 * self.P} v{vt}, {self.vp(r)} offset:{k * stride}")
+                        e(f"ds_write_b{32 * width} v{vt}, {vr} offset:{k * stride}")
                     else:
-                        e(f"ds_read_b{32 * self.P} {self.vp(r)}, v{vt} offset:{k * stride}")
+                        e(f"ds_read_b{32 * width} {vr}, v{vt} offset:{k * stride}")
                 if tag == "lo":
                     e(f"s_branch .Ltrw_{s}_{b}_{phase}done")
             self.label(f".Ltrw_{s}_{b}_{phase}done")
@@ -1075,10 +1115,10 @@ class Gen:
         # ---- handlers
         for kind in KINDS:
             for s in range(R):
-                for c in (0, 1):
+                for c in (0, 1, 2):
                     self.gen_slot(kind, s, c)
         for s in range(R):
-            for c in (0, 1):
+            for c in (0, 1, 2):
                 self.gen_d2s(s, c)
         for c in (0, 1):
             self.gen_d2l(c)
@@ -1097,7 +1137,7 @@ class Gen:
                     self.gen_lane(kind, l, c)
         for kind in KINDS2:
             for s in range(R):
-                for c in (0, 1):
+                for c in (0, 1, 2):
                     if kind == "HADD" and c:
                         continue   # only uncontrolled Hadamards drop their 1/sqrt2
                     self.gen_slot2(kind, s, c)
@@ -1324,7 +1364,7 @@ def main():
         f.write(f"static const int kWaveImageVgprs = {vg.group(1)};\n")
         set_layout(args.slots)
         f.write(f"static const int kWaveImagePrec = {args.prec};\n")
-        for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch"):
+        for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch", "slotL", "slot2L", "d2sL"):
             f.write(f"static const int kWaveIdx_{k} = {LAYOUT[k]};\n")
         f.write(f"static const int kWaveSentinelIndex = {LAYOUT['done']};\n")
         f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
