@@ -146,5 +146,6 @@ void applyProgramPerm(QuregImpl& q, const TileProgram& prog);
 // Cost in VALU instructions per lane of one transposition with lane bit l
 // (for the planner's statistics and tests).
 int waveTransposeCost(int laneBit);
+extern long long g_waveStoreTrCost;   // planner study: weighted transpositions for the store layout
 
 }  // namespace qa

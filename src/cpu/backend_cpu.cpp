@@ -526,7 +526,8 @@ static void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
         if (wp.ops[(size_t)i].kind == (int)WKind::TR) trb[wp.ops[(size_t)i].b & 15]++;
     fprintf(stderr, "wave: TR per bit:");
     for (int b = 0; b < 9; b++) fprintf(stderr, " %d", trb[b]);
-    fprintf(stderr, "\nwave: cumulative weighted transposition cost %lld\n", g_trCost);
+    fprintf(stderr, "\nwave: cumulative weighted transposition cost %lld (store layout %lld)\n", g_trCost,
+            g_waveStoreTrCost);
 }
 
 void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {
