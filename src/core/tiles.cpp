@@ -467,7 +467,8 @@ void applyPerm(std::vector<Op>& ops, const std::vector<char>& done, int first, c
 
 }  // namespace
 
-void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom) {
+void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom,
+               const PlanHooks* hooks) {
     out.passes.clear();
     out.ops.clear();
     out.perm.resize(L);
@@ -480,8 +481,12 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
     const int highSlots = k - c;
     int n = (int)ops.size();
 
+    const bool ready = hooks && hooks->passReady;
     if (!fuse) {
-        for (int i = 0; i < n; i++) emitPass(ops, i, i + 1, targetMask(ops[i]), L, k, c, out);
+        for (int i = 0; i < n; i++) {
+            emitPass(ops, i, i + 1, targetMask(ops[i]), L, k, c, out);
+            if (ready) hooks->passReady(out, i, ops);
+        }
         return;
     }
     if (fuseBlocks()) {
@@ -625,6 +630,11 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                     }
                 }
             }
+            if (choice >= 0 && hooks && hooks->relabelOk) {
+                TilePass cand = ps;
+                for (int i = 0; i < cand.k; i++) cand.stPos[i] = pis[choice][cand.pos[i]];
+                if (!hooks->relabelOk(cand, out.ops.data() + cand.opBegin)) choice = -1;
+            }
             if (choice >= 0) {
                 const int* pi = pis[choice];
                 TilePass& last = out.passes.back();
@@ -633,6 +643,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 for (int x = 0; x < L; x++) out.perm[x] = pi[out.perm[x]];
             }
         }
+        if (ready) hooks->passReady(out, (int)out.passes.size() - 1, order);
     }
     ops.swap(order);
 }

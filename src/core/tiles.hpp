@@ -15,6 +15,7 @@
 // the full state (QuEST/src/GPU/QuEST_gpu.cu, e.g. :586-592).
 #pragma once
 
+#include <functional>
 #include <vector>
 
 #include "core.hpp"
@@ -139,7 +140,19 @@ int& fuseBlockQubits();
 // so that the qubits the rest of the queue needs soonest land on the low
 // positions below cmin, which every later tile contains.  The remaining ops
 // are remapped to the new layout and out.perm records the composition.
-void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1);
+// Optional callbacks of planTiles.  relabelOk: a relabelling store layout
+// for the pass just emitted is kept only if it accepts the pass with that
+// layout (e.g. the wave engine can lower it).  passReady: called once per pass
+// as soon as it is final (its store layout decided), in program order, with
+// the scheduled ops so far (the pass's ops are order[opBegin, opEnd)) -- the
+// backend launches it while the planner works on the next pass.
+struct PlanHooks {
+    std::function<bool(const TilePass&, const TileOp*)> relabelOk;
+    std::function<void(const TileProgram&, int pass, const std::vector<Op>& order)> passReady;
+};
+
+void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,
+               const PlanHooks* hooks = nullptr);
 // Whether any pass of the program stores with a permuted layout.
 bool programRelabels(const TileProgram& prog);
 

@@ -207,6 +207,18 @@ bool relabelsLower(const TileProgram& prog) {
     return ok;
 }
 
+long long g_waveStoreTrCost = 0;
+
+bool waveLowers(const TilePass& ps, const TileOp* ops) {
+    const Stats keep = stats();
+    const long long keepTr = g_waveStoreTrCost;
+    WaveProgram tmp;
+    const bool ok = planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp);
+    stats() = keep;
+    g_waveStoreTrCost = keepTr;
+    return ok;
+}
+
 void applyProgramPerm(QuregImpl& q, const TileProgram& prog) {
     if ((int)prog.perm.size() != q.L) return;
     bool id = true;
@@ -216,8 +228,6 @@ void applyProgramPerm(QuregImpl& q, const TileProgram& prog) {
         if (q.l2p[lg] < q.L) q.l2p[lg] = prog.perm[q.l2p[lg]];
     for (int lg = 0; lg < q.nSV; lg++) q.p2l[q.l2p[lg]] = lg;
 }
-
-long long g_waveStoreTrCost = 0;
 
 int waveTransposeCost(int laneBit) { return laneBit >= kWaveLanes ? 3 : laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
 

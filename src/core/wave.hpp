@@ -140,6 +140,10 @@ bool& waveRelabel();
 // Every relabelling pass of the program lowers to the wave engine (the LDS
 // and direct kernels store in place); false -> plan again without relabelling.
 bool relabelsLower(const TileProgram& prog);
+
+// The wave engine can lower this pass (planWavePass on a scratch program; the
+// statistics are left alone): the planner's relabelOk hook.
+bool waveLowers(const TilePass& ps, const TileOp* ops);
 // After a program ran: the register's qubits moved by prog.perm.
 void applyProgramPerm(QuregImpl& q, const TileProgram& prog);
 

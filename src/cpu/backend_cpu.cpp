@@ -664,10 +664,15 @@ void flush(QuregImpl& q) {
     for (const Op& op : q.pending) channels = channels || op.kind == OpKind::Mat4 || op.kind == OpKind::DensChan2;
     const int cminWave = channels ? kWaveVecBits + 4 : waveCmin;
     const bool relabel = wave && !channels && rt().fusion && waveRelabel() && !rt().verify;
+    // as the HIP backend (streamed wave flushes): relabel only passes the wave
+    // engine lowers -- the same plans (QUEST_PLAN_STREAM=0: the fallback below)
+    static const bool streamOn = !getenv("QUEST_PLAN_STREAM") || atoi(getenv("QUEST_PLAN_STREAM")) != 0;
+    PlanHooks hooks;
+    hooks.relabelOk = [](const TilePass& ps, const TileOp* ops) { return waveLowers(ps, ops); };
     std::vector<Op> orig;
     if (relabel) orig = q.pending;
     planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminWave : 4, rt().fusion, prog,
-              relabel ? kWaveVecBits : -1);
+              relabel ? kWaveVecBits : -1, relabel && streamOn ? &hooks : nullptr);
     if (relabel && programRelabels(prog) && !relabelsLower(prog)) {
         q.pending.swap(orig);
         planTiles(q.pending, q.L, kWaveBits, cminWave, rt().fusion, prog);
