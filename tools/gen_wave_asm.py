@@ -397,19 +397,19 @@ class Gen:
         e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
         e("s_branch .Lnext")
 
-    # ---- predication: per register j, exec = lanes whose controls hold ----
+    # ---- predication: exec = lanes whose controls hold; registers j whose
+    # slot controls fail are branched over (the record's cReg word carries
+    # the host-computed mask of the registers that pass, bit j) ----
     def ctrl_begin(self):
         # LM (s[96:97]) = lanes with (lane & cLane) == cLane
         self.e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
         self.e(f"v_cmp_eq_u32_e64 s[96:97], s70, v{self.vTmp}")
         self.e("s_nop 4")
+        self.e("s_mov_b64 exec, s[96:97]")
 
     def ctrl_j(self, j, skip):
-        # exec = (j & cReg) == cReg ? LM : 0
-        self.e(f"s_and_b32 s98, s69, {j}")
-        self.e("s_cmp_eq_u32 s98, s69")
-        self.e("s_cselect_b64 exec, s[96:97], 0")
-        self.e(f"s_cbranch_execz {skip}")
+        self.e(f"s_bitcmp1_b32 s69, {j}")
+        self.e(f"s_cbranch_scc0 {skip}")
 
     def ctrl_end(self):
         self.e("s_mov_b64 exec, -1")
@@ -528,9 +528,8 @@ class Gen:
     # ---- handlers --------------------------------------------------------
     def lane_exec_begin(self):
         """ctrl 2 (controls on lane bits only): exec = the lanes whose cLane
-        bits are set, once for the whole handler."""
+        bits are set, no per-register tests."""
         self.ctrl_begin()
-        self.e("s_mov_b64 exec, s[96:97]")
 
     def gen_slot(self, kind, s, ctrl):
         self.handler(idx_slot(kind, s, ctrl), f"{kind}_s{s}_c{ctrl}")
