@@ -481,3 +481,23 @@ def test_sync_watchdog_reports_unfinished_work():
     ok = subprocess.run([sys.executable, "-c", code], cwd=root, env=envv, capture_output=True, text=True,
                         timeout=300)
     assert ok.returncode == 0 and "FINISHED" in ok.stdout, ok.stderr[-2000:]
+
+
+@pytest.mark.parametrize("stream", ["1", "0"])
+def test_relabelled_layout_reads_on_gpu(stream):
+    """GPU twin of tests/test_relabel.py: a 22-qubit layered circuit on the
+    wave engine with relabelling passes (streamed to the GPU pass by pass, or
+    planned whole first: QUEST_PLAN_STREAM), then amplitudes, marginals,
+    clones, inner products, setAmps and a checkpoint in the permuted layout,
+    all against the NumPy oracle.  Subprocess: the knob is read once."""
+    import subprocess
+    import sys
+
+    from test_relabel import ROOT, SCRIPT
+
+    out = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, "22"], cwd=ROOT, capture_output=True, text=True,
+                         timeout=240, env=dict(os.environ, QUEST_BACKEND="hip", QUEST_PLAN_STREAM=stream))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "relabel ok" in out.stdout
+    moved = int(out.stdout.split("moved")[1].split()[0])
+    assert moved > 0, out.stdout
