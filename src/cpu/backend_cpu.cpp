@@ -508,6 +508,34 @@ long long g_trCost = 0;  // QUEST_WAVE_DUMP: weighted transposition cost (planne
 static void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
     static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;
     if (!dump) return;
+    // QUEST_WAVE_DUMP=2: the GPU handler of every op (names of
+    // tools/gen_wave_asm.py, for tools/wave_cost.py)
+    static const bool perOp = atoi(getenv("QUEST_WAVE_DUMP")) == 2;
+    static const char* kName[] = {"M2", "M2R", "M2RI", "ANTI", "SWAP", "DIAG", "D2S", "D2L", "TR", "LM2R", "LM2RI",
+                                  "LANTI", "LSWAP", "ROTY", "ROTX", "HADD", "YSW", "YSWC", "DROT", "DNEG", "DMULI",
+                                  "DMULNI", "DROTN", "CH1", "CHD"};
+    for (int i = ps.opBegin; i < ps.opEnd && perOp; i++) {
+        const WaveOp& w = wp.ops[(size_t)i];
+        const unsigned lanes = w.cLane & 63u;
+        const int ctrl = (w.cReg | lanes) == 0 ? 0 : (w.cReg == 0 ? 2 : 1);
+        const char* k = kName[w.kind];
+        switch ((WKind)w.kind) {
+            case WKind::TR:
+                if (w.b < kWaveLanes) fprintf(stderr, "H wh_TR_s%d_l%d\n", w.a, w.b);
+                else fprintf(stderr, "H wh_TRW_s%d_b%d\n", w.a, w.b - kWaveLanes);
+                break;
+            case WKind::DIAG: case WKind::DROT: case WKind::DNEG: case WKind::DMULI: case WKind::DMULNI:
+            case WKind::DROTN:
+                fprintf(stderr, "H wh_%s_m%u_l%d\n", k, w.cReg, lanes ? 1 : 0);
+                break;
+            case WKind::D2L: fprintf(stderr, "H wh_D2L_c%d\n", ctrl ? 1 : 0); break;
+            case WKind::LM2R: case WKind::LM2RI: case WKind::LANTI: case WKind::LSWAP:
+                fprintf(stderr, "H wh_%s_l%d_c%d\n", k, w.a, ctrl ? 1 : 0);
+                break;
+            case WKind::CH1: case WKind::CHD: fprintf(stderr, "H wh_%s_a%d_b%d\n", k, w.a, w.b); break;
+            default: fprintf(stderr, "H wh_%s_s%d_c%d\n", k, w.a, ctrl); break;
+        }
+    }
     int cnt[32] = {0}, trw = 0, ctl = 0;
     for (int i = ps.opBegin; i < ps.opEnd; i++) {
         const WaveOp& w = wp.ops[(size_t)i];
