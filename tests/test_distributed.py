@@ -85,3 +85,21 @@ def test_wave_relabelling_with_rank_swaps(env, tmp_path, ranks):
             continue
         np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
     assert int(got["_swaps"]) > 0
+
+
+@pytest.mark.parametrize("name", ["random_ops_statevector", "calculations", "layered_wave_relabel"])
+def test_eight_ranks(env, tmp_path, name):
+    """The driver's 8-GPU shape (three rank qubits, all-to-all swaps among 8
+    ranks, k = 3) rehearsed on the host transport."""
+    want = _single(name, env)
+    extra = {"QUEST_CPU_PLANNER": "3"} if name == "layered_wave_relabel" else {}
+    got = _multi(name, 8, tmp_path, **extra)
+    assert int(got["_ranks"]) == 8
+    for k, v in want.items():
+        if k.startswith("_"):
+            continue
+        g = got[k]
+        if isinstance(v, str):
+            assert str(g) == v, k
+        else:
+            np.testing.assert_allclose(np.asarray(g), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
