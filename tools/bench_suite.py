@@ -10,6 +10,7 @@
               30 calcProbOfOutcome, 10 getAmp; tutorial_example.c), wall time
               vs its published 3783.93 s estimate
   q34         34 qubits (256 GiB state, one MI355X): single gates + 6 layers
+  qft30       30-qubit quantum Fourier transform on |+>^n (result |0>)
   density17   17-qubit density matrix (also 2^34 amplitudes) + damping on
               every qubit + gates
 
@@ -109,6 +110,31 @@ def run_random30(env, res):
     r.close()
 
 
+def run_qft30(env, res, n=30):
+    """Quantum Fourier transform (H + n(n-1)/2 controlled phases) on |+>^n:
+    the result is |0...0> (amp(0) = 1), a check as well as a timing."""
+    import quest_amd as qa
+    from quest_amd.models import qft
+    from quest_amd.ops import capi
+
+    c = qft(n)
+    r = qa.Register(env, n)
+    r.init_plus()
+    r.sync()
+    capi.resetQuESTStats()
+    t0 = time.perf_counter()
+    c.apply(r)
+    r.sync()
+    dt = time.perf_counter() - t0
+    st = capi.getQuESTStats()
+    a0 = r.amp(0)
+    res["qft30"] = {"gates": len(c.gates), "seconds": dt, "s_per_gate": dt / len(c.gates), "passes": st["passes"],
+                    "amp0_error": abs(a0 - 1)}
+    print(f"qft{n}: {len(c.gates)} gates in {dt:.3f} s ({1e3 * dt / len(c.gates):.3f} ms/gate, {st['passes']} passes), "
+          f"|amp0 - 1| = {abs(a0 - 1):.2e}", flush=True)
+    r.close()
+
+
 def run_fork30(env, res):
     import quest_amd as qa
     from quest_amd.models import fork_circuit
@@ -198,7 +224,7 @@ def run_density17(env, res, n=17):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="tutorial,sweep,random30,fork30,q34,density17")
+    ap.add_argument("--only", default="tutorial,sweep,random30,qft30,fork30,q34,density17")
     ap.add_argument("--max-qubits", type=int, default=34)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
@@ -217,6 +243,8 @@ def main():
         run_fork30(env, res)
     if "random30" in todo:
         run_random30(env, res)
+    if "qft30" in todo:
+        run_qft30(env, res)
     if "sweep" in todo:
         run_sweep(env, res, args.max_qubits)
     if "q34" in todo and args.max_qubits >= 34:
