@@ -237,8 +237,8 @@ def schedule(body):
 
 
 class Gen:
-    def __init__(self, R, dbuf, W, P=2, debug=False, stagger=0, nomem=False):
-        self.stagger = stagger
+    def __init__(self, R, dbuf, W, P=2, debug=False, nomem=False, lean=False):
+        self.lean = lean        # 80 VGPRs / half outboxes: three 8-wave workgroups per CU
         self.nomem = nomem      # experiment: no state loads / stores (compute time alone)
         self.debug = debug
         self.R = R
@@ -250,20 +250,36 @@ class Gen:
         self.dbuf = dbuf
         self.W = W               # wave bits: 2^W waves share a tile (LDS exchanges)
         self.NW = 1 << W
-        self.OUTBOX = self.NS * 64 * 4 * P   # bytes of one wave's LDS outbox (NS values x 64 lanes)
+        # bytes of one wave's LDS outbox (NS values x 64 lanes; lean: half of
+        # them, a wave-bit transposition then runs in two rounds)
+        self.OUTBOX = self.NS * 64 * 4 * P // (2 if lean else 1)
         self.lines = []
         # v[0 : 2P NS) the tile being processed (A), then the next tile being
         # loaded (B, software pipeline; dbuf only), then temporaries
         self.B = 2 * P * self.NS if dbuf else 0
         D = (2 if dbuf else 1) * 2 * P * self.NS
         self.D = D
-        # 16 temporaries (values): pairs / elements of a handler cycle
-        # through 4 / 8 sets so that the scheduler can interleave them
-        self.T = [D + P * k for k in range(16)]
-        self.C0, self.C1 = D + 16 * P, D + 17 * P
-        self.vLane, self.vLdB, self.vStB, self.vTmp = D + 18 * P, D + 18 * P + 1, D + 18 * P + 2, D + 18 * P + 3
-        self.CL = D + 18 * P + 4       # 4 values: per-lane coefficients of the lane-bit gates
-        self.nvgpr = D + 22 * P + 4    # fp64 R = 4: 112 VGPRs, 4 waves per SIMD
+        if not lean:
+            # 16 temporaries (values): pairs / elements of a handler cycle
+            # through 4 / 8 sets so that the scheduler can interleave them
+            self.NT = 16
+            self.T = [D + P * k for k in range(16)]
+            self.C0, self.C1 = D + 16 * P, D + 17 * P
+            self.vLane, self.vLdB, self.vStB, self.vTmp = D + 18 * P, D + 18 * P + 1, D + 18 * P + 2, D + 18 * P + 3
+            self.CL = D + 18 * P + 4       # 4 values: per-lane coefficients of the lane-bit gates
+            self.CLA = self.CL + 2 * P     # the anti-diagonal's pair of them
+            self.nvgpr = D + 22 * P + 4    # fp64 R = 4: 112 VGPRs, 4 waves per SIMD
+        else:
+            # 4 temporaries (every set index aliases them: the scheduler keeps
+            # the order), the lane-gate coefficients in temporaries 2-3, the
+            # lane gates one amplitude at a time: fp64 80 VGPRs, 6 waves per SIMD
+            self.NT = 4
+            self.T = [D + P * (k % 4) for k in range(16)]
+            self.C0, self.C1 = D + 4 * P, D + 5 * P
+            self.vLane, self.vLdB, self.vStB, self.vTmp = D + 6 * P, D + 6 * P + 1, D + 6 * P + 2, D + 6 * P + 3
+            self.CL = self.T[2]
+            self.CLA = self.T[2]
+            self.nvgpr = D + 6 * P + 4
         self.handlers = {}
         self.hstart = None       # first body line of the handler being generated
         self.lane_ctrl = False   # generating a ctrl-2 (lane controls only) handler
@@ -742,7 +758,7 @@ class Gen:
             for base in (self.re, self.im):
                 for d in range(self.P):
                     pairs.append((base(j) + d, base(f) + d))
-        tmp = [self.D + i for i in range(8)]   # the first 8 dwords of the temporaries
+        tmp = [self.D + i for i in range(min(8, self.NT * self.P))]   # the first dwords of the temporaries
         if l >= 4:
             op = "v_permlane32_swap_b32_e32" if l == 5 else "v_permlane16_swap_b32_e32"
             for a, b in pairs:
@@ -755,7 +771,7 @@ class Gen:
             hi_banks = "0xc" if l == 3 else "0xa"   # lanes with the bit set
             # all copies first (32 temporaries), then the DPP moves: one
             # VALU-write -> DPP-read wait for the whole handler
-            G = 16 * self.P                    # dwords of temporaries
+            G = self.NT * self.P               # dwords of temporaries
             big = [self.D + i for i in range(G)]
             for g in range(0, len(pairs), G):
                 grp = pairs[g:g + G]
@@ -771,8 +787,9 @@ class Gen:
         qp = "[1,0,3,2]" if l == 0 else "[2,3,0,1]"
         e(f"v_and_b32_e32 v{self.vTmp}, {1 << l}, v{self.vLane}")
         e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
-        for g in range(0, len(pairs), 4):
-            grp = pairs[g:g + 4]
+        per = len(tmp) // 2
+        for g in range(0, len(pairs), per):
+            grp = pairs[g:g + per]
             for k, (a, b) in enumerate(grp):
                 e(f"v_mov_b32_dpp v{tmp[2 * k]}, v{b} quad_perm:{qp} row_mask:0xf bank_mask:0xf")
                 e(f"v_mov_b32_dpp v{tmp[2 * k + 1]}, v{a} quad_perm:{qp} row_mask:0xf bank_mask:0xf")
@@ -813,8 +830,8 @@ class Gen:
             sel(CL, 0, 3)
             sel(CL + P, 1, 2)
         elif kind == "ANTI":             # m01 re,im ; m10 re,im
-            sel(CL + 2 * P, 0, 2)
-            sel(CL + 3 * P, 1, 3)
+            sel(self.CLA, 0, 2)
+            sel(self.CLA + P, 1, 3)
         elif kind == "M2":               # m00, m01, m10, m11 complex
             sel(CL, 0, 6)
             sel(CL + P, 1, 7)
@@ -838,7 +855,7 @@ class Gen:
             e(f"{self.op('fma')} {x}, {CS}, {x}, {py}")
             e(f"{self.op('fma')} {y}, {CS}, {y}, {px}")
         elif kind == "ANTI":
-            CPr, CPi = self.vp(self.CL + 2 * self.P), self.vp(self.CL + 3 * self.P)
+            CPr, CPi = self.vp(self.CLA), self.vp(self.CLA + self.P)
             e(f"{self.op('mul')} {x}, {CPr}, {px}")
             e(f"{self.op('mul')} {y}, {CPr}, {py}")
             e(f"{self.op('fma')} {x}, -{CPi}, {py}, {x}")
@@ -868,7 +885,7 @@ class Gen:
         if ctrl:
             self.ctrl_begin()
         per = 3 if kind == "M2" else 2        # temporaries (doubles) per amplitude
-        batch = 1 if ctrl else (4 if kind == "M2" else 8)
+        batch = 1 if ctrl or self.lean else (4 if kind == "M2" else 8)
         for j0 in range(0, NS, batch):
             js = list(range(j0, j0 + batch))
             skip = f".Lskip_L{kind}_{l}_{j0}"
@@ -930,26 +947,31 @@ class Gen:
         e(f"s_mul_i32 s96, s3, {ob}")
         e(f"v_lshlrev_b32_e32 v{vt}, {(4 * width).bit_length() - 1}, v{vl}")
         e(f"v_add_u32_e32 v{vt}, s96, v{vt}")
-        for phase in ("w", "r"):
-            e(f"s_bitcmp1_b32 s3, {b}")
-            e(f"s_cbranch_scc1 .Ltrw_{s}_{b}_{phase}hi")
-            for regs, tag in ((lo_regs, "lo"), (hi_regs, "hi")):
-                if tag == "hi":
-                    self.label(f".Ltrw_{s}_{b}_{phase}hi")
-                for k, r in enumerate(regs):
-                    stride = 64 * 4 * width
-                    vr = f"v[{r}:{r + width - 1}]" if width > 1 else f"v{r}"
-                    if phase == "w":
-                        e(f"ds_write_b{32 * width} v{vt}, {vr} offset:{k * stride}")
-                    else:
-                        e(f"ds_read_b{32 * width} {vr}, v{vt} offset:{k * stride}")
-                if tag == "lo":
-                    e(f"s_branch .Ltrw_{s}_{b}_{phase}done")
-            self.label(f".Ltrw_{s}_{b}_{phase}done")
-            if phase == "w":
-                e(f"v_xor_b32_e32 v{vt}, {(1 << b) * ob}, v{vt}")   # the partner's outbox
-            e("s_waitcnt lgkmcnt(0)")
-            e("s_barrier")
+        # lean: the outbox holds half of the moved registers, two rounds
+        rounds = 2 if self.lean else 1
+        per = len(lo_regs) // rounds
+        for rnd in range(rounds):
+            for phase in ("w", "r"):
+                tagp = f"{rnd}{phase}"
+                e(f"s_bitcmp1_b32 s3, {b}")
+                e(f"s_cbranch_scc1 .Ltrw_{s}_{b}_{tagp}hi")
+                for regs, tag in ((lo_regs, "lo"), (hi_regs, "hi")):
+                    if tag == "hi":
+                        self.label(f".Ltrw_{s}_{b}_{tagp}hi")
+                    for k, r in enumerate(regs[rnd * per:(rnd + 1) * per]):
+                        stride = 64 * 4 * width
+                        vr = f"v[{r}:{r + width - 1}]" if width > 1 else f"v{r}"
+                        if phase == "w":
+                            e(f"ds_write_b{32 * width} v{vt}, {vr} offset:{k * stride}")
+                        else:
+                            e(f"ds_read_b{32 * width} {vr}, v{vt} offset:{k * stride}")
+                    if tag == "lo":
+                        e(f"s_branch .Ltrw_{s}_{b}_{tagp}done")
+                self.label(f".Ltrw_{s}_{b}_{tagp}done")
+                if phase == "w" or rnd + 1 < rounds:
+                    e(f"v_xor_b32_e32 v{vt}, {(1 << b) * ob}, v{vt}")   # the partner's outbox (and back)
+                e("s_waitcnt lgkmcnt(0)")
+                e("s_barrier")
         self.back()
 
     # ---- the kernel -------------------------------------------------------
@@ -996,7 +1018,7 @@ class Gen:
         # first tile of this workgroup.  The dispatcher deals workgroups to the
         # 8 XCDs round-robin, then to the CUs of an XCD, then a second round
         # (P per CU): with the host's map word (launch + 20: bit 31 enable,
-        # bits 0-7 log2 CUs per XCD, 8-15 log2 P) workgroup w takes tile
+        # bits 0-7 log2 CUs per XCD, 8-15 P) workgroup w takes tile
         # (w % 8) * C * P + ((w / 8) % C) * P + w / (8 C): the P workgroups of
         # a CU take adjacent tiles and an XCD a contiguous block -- they share
         # pages (address translations) instead of each touching its own
@@ -1006,34 +1028,18 @@ class Gen:
         e("s_bitcmp1_b32 s99, 31")
         e("s_cbranch_scc0 .Lmap_done")
         e("s_bfe_u32 s97, s99, 0x80000")             # log2 C (bits 0-7)
-        e("s_bfe_u32 s96, s99, 0x80008")             # log2 P (bits 8-15)
+        e("s_bfe_u32 s96, s99, 0x80008")             # P (bits 8-15; any value, e.g. 3)
         e("s_lshr_b32 s98, s2, 3")                   # r = w / 8
         e("s_bfm_b32 s95, s97, 0")                   # C - 1
         e("s_and_b32 s95, s98, s95")                 # cu = r % C
         e("s_lshr_b32 s98, s98, s97")                # slot = r / C
-        e("s_lshl_b32 s95, s95, s96")                # cu * P
+        e("s_mul_i32 s95, s95, s96")                 # cu * P
         e("s_add_u32 s98, s98, s95")                 # cu * P + slot
-        e("s_add_u32 s95, s97, s96")                 # log2 (C P)
+        e("s_lshl_b32 s95, s96, s97")                # C P
         e("s_and_b32 s16, s2, 7")
-        e("s_lshl_b32 s16, s16, s95")                # (w % 8) C P
+        e("s_mul_i32 s16, s16, s95")                 # (w % 8) C P
         e("s_add_u32 s16, s16, s98")
         self.label(".Lmap_done")
-        if self.stagger:
-            # experiment: the odd workgroup of a CU starts `stagger` x 8128
-            # cycles late, so the two resident tiles of a CU run out of phase
-            # (one loading or storing while the other computes)
-            e("s_bfe_u32 s97, s99, 0x80000")
-            e("s_lshr_b32 s98, s2, 3")
-            e("s_lshr_b32 s98, s98, s97")
-            e("s_bitcmp1_b32 s98, 0")
-            e("s_cbranch_scc0 .Lstagger_done")
-            e(f"s_mov_b32 s98, {self.stagger}")
-            self.label(".Lstagger")
-            e("s_sleep 127")
-            e("s_sub_u32 s98, s98, 1")
-            e("s_cmp_lg_u32 s98, 0")
-            e("s_cbranch_scc1 .Lstagger")
-            self.label(".Lstagger_done")
         e("s_mov_b32 s17, 0")
         e("s_waitcnt vmcnt(0) lgkmcnt(0)")
         if self.dbuf:
@@ -1327,8 +1333,8 @@ def main():
     ap.add_argument("--dbuf", type=int, default=-1, help="software-pipelined tiles (default: when 4 slots)")
     ap.add_argument("--wbits", type=int, default=3, help="2^wbits waves share a tile")
     ap.add_argument("--debug", action="store_true", help="record addressing state per wave and stop (no state access)")
-    ap.add_argument("--stagger", type=int, default=0, help="start odd workgroups of a CU N x 8128 cycles late")
     ap.add_argument("--nomem", action="store_true", help="experiment: drop the state loads and stores")
+    ap.add_argument("--lean", type=int, default=0, help="1: 80-VGPR layout, half outboxes (3 workgroups per CU)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--obj")
     ap.add_argument("--hsaco")
@@ -1338,7 +1344,7 @@ def main():
         # a tile has <= 4 waves (otherwise too few workgroups fit a CU)
         dbuf = args.dbuf if args.dbuf >= 0 else (args.slots <= 4 and args.wbits <= 2)
         set_layout(args.slots)
-        g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug, args.stagger, args.nomem)
+        g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug, args.nomem, bool(args.lean))
         g.kernel()
         with open(args.out, "w") as f:
             f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
