@@ -277,8 +277,8 @@ class Gen:
             self.T = [D + P * (k % 4) for k in range(16)]
             self.C0, self.C1 = D + 4 * P, D + 5 * P
             self.vLane, self.vLdB, self.vStB, self.vTmp = D + 6 * P, D + 6 * P + 1, D + 6 * P + 2, D + 6 * P + 3
-            self.CL = self.T[2]
-            self.CLA = self.T[2]
+            self.CL = self.C0             # lane-gate coefficients in C0 / C1 (scratch: vTmp)
+            self.CLA = self.C0
             self.nvgpr = D + 6 * P + 4
         self.handlers = {}
         self.hstart = None       # first body line of the handler being generated
@@ -822,6 +822,12 @@ class Gen:
 
         def sel(dst, k_clear, k_set):
             e(f"{self.MOV} {self.vp(dst)}, {self.sm(k_clear)}")
+            if self.lean:
+                # the coefficients live in C0 / C1: select dword by dword through vTmp
+                for d in range(self.P):
+                    e(f"v_mov_b32_e32 v{self.vTmp}, s{76 + self.P * k_set + d}")
+                    e(f"v_cndmask_b32_e32 v{dst + d}, v{dst + d}, v{self.vTmp}, vcc")
+                return
             e(f"{self.MOV} {self.vp(C0)}, {self.sm(k_set)}")
             for d in range(self.P):
                 e(f"v_cndmask_b32_e32 v{dst + d}, v{dst + d}, v{C0 + d}, vcc")
@@ -885,7 +891,7 @@ class Gen:
         if ctrl:
             self.ctrl_begin()
         per = 3 if kind == "M2" else 2        # temporaries (doubles) per amplitude
-        batch = 1 if ctrl or self.lean else (4 if kind == "M2" else 8)
+        batch = 1 if ctrl else (2 if self.lean else (4 if kind == "M2" else 8))
         for j0 in range(0, NS, batch):
             js = list(range(j0, j0 + batch))
             skip = f".Lskip_L{kind}_{l}_{j0}"
