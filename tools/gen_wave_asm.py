@@ -69,6 +69,9 @@ CH_KINDS = ["CH1", "CHD"]
 
 LAYOUT = {}
 SWAP64 = _os.environ.get("WAVE_SWAP64", "1") == "1"   # register exchanges as 64-bit moves (swap_vals)
+# per-lane selects: v_cmp_*_e64 into this SGPR pair + v_cndmask_b32_e64 (a
+# v_cndmask_b32_e32 reading vcc issues ~5x slower on gfx950, tools/isa_micro.hip)
+SEL = "s[98:99]"
 
 
 # op record fields live in s[36:59] (prefetch buffer) and s[68:91] (the
@@ -146,7 +149,7 @@ def table_size(R):
     return LAYOUT["done"] + 1
 
 
-_VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b|\b(vcc)\b")
+_VREG = re.compile(r"v\[(\d+):(\d+)\]|\bv(\d+)\b|\b(vcc)\b|(s\[98:99\])")
 
 
 def _regs(operand):
@@ -156,8 +159,10 @@ def _regs(operand):
             out.update(range(int(m.group(1)), int(m.group(2)) + 1))
         elif m.group(3):
             out.add(int(m.group(3)))
-        else:
+        elif m.group(4):
             out.add("vcc")
+        else:
+            out.add("sel")   # the SEL mask pair
     return out
 
 
@@ -700,7 +705,7 @@ class Gen:
         self.handler(idx_d2l(ctrl), f"D2L_c{ctrl}")
         # per-lane coefficient: lane bit aux (s71) ? d1 : d0
         self.e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, s71, 1")
-        self.e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
+        self.e(f"v_cmp_ne_u32_e64 {SEL}, 0, v{self.vTmp}")
         C0, C1, T0, T1 = self.C0, self.C1, self.T[14], self.T[15]
         self.e(f"{self.MOV} {self.vp(C0)}, {self.sm(0)}")
         self.e(f"{self.MOV} {self.vp(C1)}, {self.sm(1)}")
@@ -708,7 +713,7 @@ class Gen:
         self.e(f"{self.MOV} {self.vp(T1)}, {self.sm(3)}")
         for c, t in ((C0, T0), (C1, T1)):
             for d in range(self.P):
-                self.e(f"v_cndmask_b32_e32 v{c + d}, v{c + d}, v{t + d}, vcc")
+                self.e(f"v_cndmask_b32_e64 v{c + d}, v{c + d}, v{t + d}, {SEL}")
         if ctrl:
             self.ctrl_begin()
         else:
@@ -743,18 +748,18 @@ class Gen:
             return
         C0, C1 = self.C0, self.C1
         e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
-        e(f"v_cmp_eq_u32_e32 vcc, s70, v{self.vTmp}")
+        e(f"v_cmp_eq_u32_e64 {SEL}, s70, v{self.vTmp}")
         e(f"{self.MOV} {self.vp(C0)}, {self.sm(0)}")
         e(f"{self.MOV} {self.vp(C1)}, {self.sm(1)}")
         if self.P == 2:
-            e(f"v_cndmask_b32_e32 v{C0}, 0, v{C0}, vcc")
-            e(f"v_mov_b32_e32 v{self.vTmp}, 0x3ff00000")   # hi dword of 1.0 (literal + vcc: two constant-bus reads)
-            e(f"v_cndmask_b32_e32 v{C0 + 1}, v{self.vTmp}, v{C0 + 1}, vcc")
-            e(f"v_cndmask_b32_e32 v{C1}, 0, v{C1}, vcc")
-            e(f"v_cndmask_b32_e32 v{C1 + 1}, 0, v{C1 + 1}, vcc")
+            e(f"v_cndmask_b32_e64 v{C0}, 0, v{C0}, {SEL}")
+            e(f"v_mov_b32_e32 v{self.vTmp}, 0x3ff00000")   # hi dword of 1.0 (a literal cannot ride in VOP3)
+            e(f"v_cndmask_b32_e64 v{C0 + 1}, v{self.vTmp}, v{C0 + 1}, {SEL}")
+            e(f"v_cndmask_b32_e64 v{C1}, 0, v{C1}, {SEL}")
+            e(f"v_cndmask_b32_e64 v{C1 + 1}, 0, v{C1 + 1}, {SEL}")
         else:
-            e(f"v_cndmask_b32_e32 v{C0}, 1.0, v{C0}, vcc")
-            e(f"v_cndmask_b32_e32 v{C1}, 0, v{C1}, vcc")
+            e(f"v_cndmask_b32_e64 v{C0}, 1.0, v{C0}, {SEL}")
+            e(f"v_cndmask_b32_e64 v{C1}, 0, v{C1}, {SEL}")
         self.region()
         for k, j in enumerate(js):
             self.cmul_vgpr(j, C0, C1, k % 8)
@@ -806,7 +811,7 @@ class Gen:
             return
         qp = "[1,0,3,2]" if l == 0 else "[2,3,0,1]"
         e(f"v_and_b32_e32 v{self.vTmp}, {1 << l}, v{self.vLane}")
-        e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
+        e(f"v_cmp_ne_u32_e64 {SEL}, 0, v{self.vTmp}")
         per = len(tmp) // 2
         for g in range(0, len(pairs), per):
             grp = pairs[g:g + per]
@@ -815,8 +820,8 @@ class Gen:
                 e(f"v_mov_b32_dpp v{tmp[2 * k + 1]}, v{a} quad_perm:{qp} row_mask:0xf bank_mask:0xf")
             for k, (a, b) in enumerate(grp):
                 # bit set: a <- partner's b ; bit clear: b <- partner's a
-                e(f"v_cndmask_b32_e32 v{a}, v{a}, v{tmp[2 * k]}, vcc")
-                e(f"v_cndmask_b32_e32 v{b}, v{tmp[2 * k + 1]}, v{b}, vcc")
+                e(f"v_cndmask_b32_e64 v{a}, v{a}, v{tmp[2 * k]}, {SEL}")
+                e(f"v_cndmask_b32_e64 v{b}, v{tmp[2 * k + 1]}, v{b}, {SEL}")
             # the next group's DPPs read other registers: no hazard
         self.back()
 
@@ -833,11 +838,11 @@ class Gen:
         self.e(f"v_mov_b32_dpp v{dst}, v{src} row_shr:{sh} row_mask:0xf bank_mask:{hi}")
 
     def lane_coeffs(self, kind, l):
-        """Per-lane coefficients (vcc = lanes with bit l set): CS multiplies
+        """Per-lane coefficients (SEL = lanes with bit l set): CS multiplies
         the lane's own amplitude, CP the partner's."""
         e = self.e
         e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, {l}, 1")
-        e(f"v_cmp_ne_u32_e32 vcc, 0, v{self.vTmp}")
+        e(f"v_cmp_ne_u32_e64 {SEL}, 0, v{self.vTmp}")
         CL, C0 = self.CL, self.C0
 
         def sel(dst, k_clear, k_set):
@@ -846,11 +851,11 @@ class Gen:
                 # the coefficients live in C0 / C1: select dword by dword through vTmp
                 for d in range(self.P):
                     e(f"v_mov_b32_e32 v{self.vTmp}, s{76 + self.P * k_set + d}")
-                    e(f"v_cndmask_b32_e32 v{dst + d}, v{dst + d}, v{self.vTmp}, vcc")
+                    e(f"v_cndmask_b32_e64 v{dst + d}, v{dst + d}, v{self.vTmp}, {SEL}")
                 return
             e(f"{self.MOV} {self.vp(C0)}, {self.sm(k_set)}")
             for d in range(self.P):
-                e(f"v_cndmask_b32_e32 v{dst + d}, v{dst + d}, v{C0 + d}, vcc")
+                e(f"v_cndmask_b32_e64 v{dst + d}, v{dst + d}, v{C0 + d}, {SEL}")
         P = self.P
         if kind in ("M2R", "M2RI"):      # m00 m01 m10 m11 (M2RI: the off-diagonals imaginary)
             sel(CL, 0, 3)
