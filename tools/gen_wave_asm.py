@@ -578,21 +578,45 @@ class Gen:
             self.ctrl_begin()
         else:
             self.region()
-        for p, j in enumerate([j for j in range(self.NS) if not (j >> s) & 1]):
-            f = j | (1 << s)
-            if ctrl:
-                skip = f".Lskip_{kind}_{s}_{j}"
-                self.ctrl_j(j, skip)
-                self.pair(kind, j, f)
-                self.label(skip)
-            else:
-                self.pair(kind, j, f, p % 4)
+        if self.P == 1 and kind == "SWAP" and not ctrl and SWAP64:
+            self.swap_pairs32(s)
+        else:
+            for p, j in enumerate([j for j in range(self.NS) if not (j >> s) & 1]):
+                f = j | (1 << s)
+                if ctrl:
+                    skip = f".Lskip_{kind}_{s}_{j}"
+                    self.ctrl_j(j, skip)
+                    self.pair(kind, j, f)
+                    self.label(skip)
+                else:
+                    self.pair(kind, j, f, p % 4)
         if ctrl:
             self.ctrl_end()
         else:
             self.end_region()
         self.lane_ctrl_end()
         self.back()
+
+    def swap_pairs32(self, s):
+        """fp32 X on slot s, every register pair: adjacent values move as 64-bit
+        pairs (s >= 1: registers j, j+1 with j and j + 2^s; s = 0: the two
+        halves of one 64-bit register, one v_pk_mov_b32)."""
+        e = self.e
+        for base in (self.re, self.im):
+            if s == 0:
+                for j in range(0, self.NS, 2):
+                    r = base(j)
+                    e(f"v_pk_mov_b32 v[{r}:{r + 1}], v[{r}:{r + 1}], v[{r}:{r + 1}] op_sel:[1,0]")
+                continue
+            for j in range(0, self.NS, 2):
+                if (j >> s) & 1:
+                    continue
+                a, b = base(j), base(j | (1 << s))
+                t = self.T[self.swap_tmp % (self.NT // 2) * 2]   # two adjacent fp32 temporaries
+                self.swap_tmp += 1
+                e(f"v_mov_b64 v[{t}:{t + 1}], v[{a}:{a + 1}]")
+                e(f"v_mov_b64 v[{a}:{a + 1}], v[{b}:{b + 1}]")
+                e(f"v_mov_b64 v[{b}:{b + 1}], v[{t}:{t + 1}]")
 
     def lane_ctrl_end(self):
         if self.lane_ctrl:
@@ -930,8 +954,12 @@ class Gen:
                             self.lane_fetch(l, r, r)
                     else:
                         tmp = [self.D + k for k in range(2 * self.P)]
-                        for r, t in zip(regs, tmp):
-                            e(f"v_mov_b32_e32 v{t}, v{r}")
+                        if self.P == 2:   # re and im as 64-bit copies
+                            e(f"v_mov_b64 v[{tmp[0]}:{tmp[1]}], v[{regs[0]}:{regs[1]}]")
+                            e(f"v_mov_b64 v[{tmp[2]}:{tmp[3]}], v[{regs[2]}:{regs[3]}]")
+                        else:
+                            for r, t in zip(regs, tmp):
+                                e(f"v_mov_b32_e32 v{t}, v{r}")
                         e("s_nop 1")
                         for r, t in zip(regs, tmp):
                             self.lane_fetch(l, r, t)
