@@ -14,6 +14,19 @@ import collections
 import re
 
 
+def issue_cycles(op, text):
+    """Wave-cycles per SIMD of one VALU instruction on gfx950, measured by
+    tools/isa_micro.hip (profiles/r2/isa_micro_gfx950.txt)."""
+    if op.startswith("v_swap") or "permlane" in op:
+        return 8.2
+    if op.startswith("v_cndmask") and "vcc" in text:
+        return 22.6
+    if "f64" in op or "b64" in op or op.startswith("v_pk_") or "_dpp" in op or op.startswith("v_cndmask") \
+            or op.startswith("v_bfi"):
+        return 4.3
+    return 2.7
+
+
 def handler_costs(path):
     cost = collections.defaultdict(collections.Counter)
     cur = None
@@ -28,6 +41,7 @@ def handler_costs(path):
         op = t.split()[0]
         if op.startswith("v_"):
             cost[cur]["valu_f64" if "f64" in op else "valu"] += 1
+            cost[cur]["cycles"] += issue_cycles(op, t)
         elif op.startswith("s_"):
             cost[cur]["salu"] += 1
         elif op.startswith("ds_"):
@@ -65,14 +79,15 @@ def main():
     for f in fam:
         tot.update(fam[f])
     print(f"{len(passes)} passes; per pass (per wave and tile):")
-    print(f"{'family':16s} {'ops':>6s} {'valu':>8s} {'f64':>8s} {'salu':>8s} {'lds':>6s}")
-    for f in sorted(fam, key=lambda f: -(fam[f]["valu"] + fam[f]["valu_f64"])):
+    print(f"{'family':16s} {'ops':>6s} {'valu':>8s} {'f64':>8s} {'cycles':>8s} {'salu':>8s} {'lds':>6s}")
+    for f in sorted(fam, key=lambda f: -fam[f]["cycles"]):
         c = fam[f]
         P = len(passes)
-        print(f"{f:16s} {n[f] / P:6.1f} {c['valu'] / P:8.0f} {c['valu_f64'] / P:8.0f} {c['salu'] / P:8.0f} {c['lds'] / P:6.0f}")
+        print(f"{f:16s} {n[f] / P:6.1f} {c['valu'] / P:8.0f} {c['valu_f64'] / P:8.0f} {c['cycles'] / P:8.0f} "
+              f"{c['salu'] / P:8.0f} {c['lds'] / P:6.0f}")
     P = len(passes)
     print(f"{'total':16s} {sum(n.values()) / P:6.1f} {tot['valu'] / P:8.0f} {tot['valu_f64'] / P:8.0f} "
-          f"{tot['salu'] / P:8.0f} {tot['lds'] / P:6.0f}")
+          f"{tot['cycles'] / P:8.0f} {tot['salu'] / P:8.0f} {tot['lds'] / P:6.0f}")
 
 
 if __name__ == "__main__":
