@@ -364,11 +364,179 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     for (int l = 0; l < kWaveLaneBits; l++) wp.ldLane[l] = lay.laneBit[l];
 
     wp.opBegin = (int)out.ops.size();
+    // Exchange frame: an uncontrolled X on a tile bit (not a vector bit) is
+    // not executed; the bit is marked flipped (F) -- its amplitude pairs sit
+    // in each other's places, wherever the bit moves (slots, lanes, waves).
+    // Later gates on a flipped bit take X M X (same handler, conjugated
+    // matrix); controls on flipped bits test for 0 (register masks computed by
+    // the host, lane masks through the record's aux word, wave bits swapped
+    // between cLane and cLaneZero); phases on a flipped register bit split in
+    // two (p on the mask without it, 1/p on the whole mask); channels and
+    // unnormalised Hadamards get the exchange first.  What is left at the end
+    // of the pass is folded into the store addresses (WavePass::stFlip*).
+    // QUEST_WAVE_XFRAME=0 executes every X.
+    static const bool frameOn = !getenv("QUEST_WAVE_XFRAME") || atoi(getenv("QUEST_WAVE_XFRAME")) != 0;
+    unsigned F = 0;
+    Scale sig;
+    auto slotFlips = [&]() {
+        unsigned m = 0;
+        for (int s = 0; s < kWaveSlots; s++) m |= ((F >> lay.slotBit[s]) & 1u) << s;
+        return m;
+    };
+    auto laneFlips = [&]() {   // real lanes and wave bits, as cLane bits
+        unsigned m = 0;
+        for (int l = 0; l < kWaveLaneBits; l++) m |= ((F >> lay.laneBit[l]) & 1u) << l;
+        return m;
+    };
+    auto materialize = [&](unsigned slots) {
+        for (unsigned m = slots & slotFlips(); m; m &= m - 1) {
+            WaveOp x = blank((int)WKind::SWAP);
+            x.a = __builtin_ctz(m);
+            out.ops.push_back(x);
+            F &= ~(1u << lay.slotBit[x.a]);
+        }
+    };
+    // the unit phase p of a phase op (DIAG: its complex factor)
+    auto phaseOf = [](const WaveOp& w, double& pr, double& pi) {
+        const double t = w.m[0], sn = w.m[1], c = 1 - t * sn;
+        switch ((WKind)w.kind) {
+            case WKind::DROT: pr = c, pi = sn; break;
+            case WKind::DROTN: pr = -c, pi = -sn; break;
+            case WKind::DNEG: pr = -1, pi = 0; break;
+            case WKind::DMULI: pr = 0, pi = 1; break;
+            case WKind::DMULNI: pr = 0, pi = -1; break;
+            default: pr = w.m[0], pi = w.m[1]; break;   // DIAG
+        }
+    };
+    auto invertPhase = [](WaveOp& w) {   // p -> 1/p
+        switch ((WKind)w.kind) {
+            case WKind::DROT:
+            case WKind::DROTN:
+                w.m[0] = -w.m[0];
+                w.m[1] = -w.m[1];
+                break;
+            case WKind::DMULI: w.kind = (int)WKind::DMULNI; break;
+            case WKind::DMULNI: w.kind = (int)WKind::DMULI; break;
+            case WKind::DNEG: break;
+            default: {   // DIAG
+                const double r = w.m[0], i = w.m[1], n = r * r + i * i;
+                w.m[0] = (real)(r / n);
+                w.m[1] = (real)(-i / n);
+            }
+        }
+    };
+    auto emit = [&](WaveOp w) {
+        const bool free = w.cReg == 0 && w.cLane == 0 && w.cLaneZero == 0 && w.ctrlOut == 0;
+        if (frameOn && free && w.kind == (int)WKind::SWAP && w.a >= VB) {
+            F ^= 1u << lay.slotBit[w.a];
+            return;
+        }
+        if (frameOn && free && w.kind == (int)WKind::LSWAP) {
+            F ^= 1u << lay.laneBit[w.a];
+            return;
+        }
+        if (!F) {
+            out.ops.push_back(w);
+            return;
+        }
+        const unsigned fs = slotFlips(), fl = laneFlips();
+        const bool isPhase = w.kind == (int)WKind::DIAG || (w.kind >= (int)WKind::DROT && w.kind <= (int)WKind::DROTN);
+        if (isPhase) {
+            const unsigned T = w.cReg & fs;
+            if (T && (__builtin_popcount(T) > 1 || (w.kind == (int)WKind::DIAG && w.m[0] == 0 && w.m[1] == 0)))
+                materialize(T);
+            else if (T) {
+                WaveOp rest = w;
+                rest.cReg &= ~T;
+                if (rest.cReg == 0 && rest.cLane == 0 && rest.cLaneZero == 0 && rest.ctrlOut == 0) {
+                    double pr, pi;
+                    phaseOf(rest, pr, pi);
+                    sig.mul(pr, pi);   // a global factor: absorbed by the pass
+                } else {
+                    rest.fLane = fl & 63u;
+                    const unsigned wv = (fl >> kWaveLanes) << kWaveLanes;
+                    const unsigned one = rest.cLane & wv, zero = rest.cLaneZero & wv;
+                    rest.cLane = (rest.cLane & ~wv) | zero;
+                    rest.cLaneZero = (rest.cLaneZero & ~wv) | one;
+                    out.ops.push_back(rest);
+                }
+                invertPhase(w);   // 1/p on the whole mask (physical bits, no flips)
+            }
+        }
+        const bool slotFlipped = inSlot(w.a) && ((fs >> w.a) & 1);
+        auto swapPairs = [&](int x, int y, int n) {
+            for (int k = 0; k < n; k++) std::swap(w.m[x + k], w.m[y + k]);
+        };
+        switch ((WKind)w.kind) {
+            case WKind::TR: break;   // the flip travels with the tile bit
+            case WKind::CH1:
+            case WKind::CHD: materialize((1u << w.a) | (1u << w.b)); break;
+            case WKind::HADD:
+                // on a flipped slot: H gives (a0 + a1, -(a0 - a1)) in (low, high), the
+                // logical order with the high half negated: clear the flip, then Z
+                if (slotFlipped) {
+                    F &= ~(1u << lay.slotBit[w.a]);
+                    out.ops.push_back(w);
+                    WaveOp z = blank((int)WKind::DNEG);   // the slot is unflipped now: no frame work
+                    z.cReg = 1u << w.a;
+                    out.ops.push_back(z);
+                    return;
+                }
+                break;
+            case WKind::M2:   // X M X: m00 <-> m11, m01 <-> m10 (complex)
+                if (slotFlipped) {
+                    swapPairs(0, 6, 2);
+                    swapPairs(2, 4, 2);
+                }
+                break;
+            case WKind::M2R:
+            case WKind::M2RI:   // (m00, m01, m10, m11) -> (m11, m10, m01, m00)
+                if (slotFlipped) {
+                    std::swap(w.m[0], w.m[3]);
+                    std::swap(w.m[1], w.m[2]);
+                }
+                break;
+            case WKind::LM2R:
+            case WKind::LM2RI:
+                if ((fl >> w.a) & 1) {
+                    std::swap(w.m[0], w.m[3]);
+                    std::swap(w.m[1], w.m[2]);
+                }
+                break;
+            case WKind::ANTI:   // m01 <-> m10
+            case WKind::D2S:    // d0 <-> d1
+                if (slotFlipped) swapPairs(0, 2, 2);
+                break;
+            case WKind::LANTI:
+            case WKind::D2L:
+                if ((fl >> w.a) & 1) swapPairs(0, 2, 2);
+                break;
+            case WKind::ROTY:   // X Ry(phi) X = Ry(-phi)
+                if (slotFlipped) {
+                    w.m[0] = -w.m[0];
+                    w.m[1] = -w.m[1];
+                }
+                break;
+            case WKind::YSW:
+            case WKind::YSWC:   // X Y X = -Y
+                if (slotFlipped) w.kind = w.kind == (int)WKind::YSW ? (int)WKind::YSWC : (int)WKind::YSW;
+                break;
+            default: break;   // ROTX, SWAP, LSWAP commute with X; phases handled above
+        }
+        // controls on flipped bits
+        if (!isPhase) w.fReg = slotFlips() & w.cReg;
+        w.fLane = laneFlips() & w.cLane & 63u;
+        const unsigned wv = ((laneFlips() >> kWaveLanes) << kWaveLanes);
+        const unsigned one = w.cLane & wv, zero = w.cLaneZero & wv;
+        w.cLane = (w.cLane & ~wv) | zero;
+        w.cLaneZero = (w.cLaneZero & ~wv) | one;
+        out.ops.push_back(w);
+    };
     auto transpose = [&](int s, int l) {
         WaveOp w = blank((int)WKind::TR);
         w.a = s;
         w.b = l;
-        out.ops.push_back(w);
+        emit(w);
         const int bs = lay.slotBit[s], bl = lay.laneBit[l];
         lay.put(bs, kWaveSlots + l);
         lay.put(bl, s);
@@ -379,7 +547,6 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // end by one uncontrolled op whose matrix can take them at no cost (or a
     // final phase op).  QUEST_WAVE_CHEAP=0 keeps the round-1 kinds only.
     static const bool cheap = !getenv("QUEST_WAVE_CHEAP") || atoi(getenv("QUEST_WAVE_CHEAP")) != 0;
-    Scale sig;
     auto uncontrolled = [&](const TileOp& op) { return op.ctrlIn == 0 && op.ctrlOut == 0; };
     // an uncontrolled general 2x2 absorbs any factor: then every uncontrolled
     // diagonal gate can drop its global phase; otherwise the first one stays
@@ -398,7 +565,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         w.ctrlOut = op.ctrlOut;
         w.m[0] = pm[0];
         w.m[1] = pm[1];
-        out.ops.push_back(w);
+        emit(w);
         return true;
     };
     // bring tile bit b into a register slot (not the slot `keep`), evicting
@@ -433,7 +600,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             w.m[2] = m[2 * 12];
             w.m[3] = m[2 * 15];
             w.m[4] = m[2 * 5];
-            out.ops.push_back(w);
+            emit(w);
             continue;
         }
         if ((OpKind)op.kind == OpKind::Diag) {
@@ -443,7 +610,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             w.ctrlOut = op.ctrlOut;
             w.m[0] = op.m[0];
             w.m[1] = op.m[1];
-            out.ops.push_back(w);
+            emit(w);
             continue;
         }
         const int t = op.t[0];
@@ -475,7 +642,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                     d.m[0] = m[v ? 6 : 0];
                     d.m[1] = m[v ? 7 : 1];
                     d.ctrlOut = op.ctrlOut;
-                    out.ops.push_back(d);
+                    emit(d);
                 }
                 continue;
             } else {
@@ -490,7 +657,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 if (uncontrolled(op)) haveComplexAbsorber = true;  // later diagonals may split
             }
             w.ctrlOut = op.ctrlOut;
-            out.ops.push_back(w);
+            emit(w);
             continue;
         }
         if (!inSlot(lay.where[t]) && laneOf(lay.where[t]) < kWaveLaneOps && cls[i] != M2Class::General &&
@@ -523,7 +690,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             w.a = laneOf(lay.where[t]);
             masks(lay, op.ctrlIn, w.cReg, w.cLane);
             w.ctrlOut = op.ctrlOut;
-            out.ops.push_back(w);
+            emit(w);
             continue;
         }
         // target into a slot (slot 0 keeps tile bit 0 for the whole pass)
@@ -604,7 +771,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         w.a = lay.where[t];
         masks(lay, op.ctrlIn, w.cReg, w.cLane);
         w.ctrlOut = op.ctrlOut;
-        out.ops.push_back(w);
+        emit(w);
     }
     if (!sig.one()) settleScale(out, wp.opBegin, sig.re, sig.im);
     // store layout: the tile bits STORED to positions VB..VB+2 on lane bits
@@ -642,6 +809,9 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         transpose(s, l);
     }
     for (size_t o = trBeforeStore; o < out.ops.size(); o++) g_waveStoreTrCost += waveTransposeCost(out.ops[o].b);
+    // flips still pending: folded into the store offsets
+    wp.stFlip = slotFlips();
+    wp.stFlipLane = laneFlips();
     for (int s = 0; s < kWaveSlots; s++) wp.stSlot[s] = lay.slotBit[s];
     for (int l = 0; l < kWaveLaneBits; l++) wp.stLane[l] = lay.laneBit[l];
     wp.opEnd = (int)out.ops.size();

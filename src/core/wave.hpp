@@ -109,6 +109,10 @@ struct WaveOp {
     unsigned cReg;    // register slots that must be 1
     unsigned cLane;   // lane bits that must be 1 (bits >= 6: wave bits)
     unsigned cLaneZero;  // lane bits that must be 0 (wave bits only)
+    // controls on tile bits the pass has flipped (deferred X, see
+    // planWavePass): register j passes when ((j ^ fReg) & cReg) == cReg,
+    // lane L when ((L ^ fLane) & cLane) == cLane (real lane bits)
+    unsigned fReg, fLane;
     u64 ctrlOut;      // physical bits outside the tile that must be 1
     real m[8];
 };
@@ -120,6 +124,11 @@ struct WavePass {
     int ldSlot[kWaveSlots];    // tile bit held by slot s at load
     int ldLane[kWaveLaneBits]; // tile bit held by lane bit l at load (l >= 6: wave bits)
     int stSlot[kWaveSlots];    // ... at store
+    // tile bits flipped at the end of the pass (X the planner did not
+    // execute, planWavePass): register j of lane L is stored where register
+    // j ^ stFlip of lane L ^ stFlipLane belongs (stFlipLane: real lane bits
+    // 0-5 and the wave bits above them)
+    unsigned stFlip = 0, stFlipLane = 0;
     int stLane[kWaveLaneBits];
 };
 

@@ -345,10 +345,10 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         const int a = w.a;
         for (int L0 = 0; L0 < kVLanes; L0++) {
             if ((L0 >> a) & 1) continue;
-            if (((unsigned)L0 & w.cLane) != w.cLane || ((unsigned)L0 & w.cLaneZero)) continue;
+            if ((((unsigned)L0 ^ w.fLane) & w.cLane) != w.cLane || ((unsigned)L0 & w.cLaneZero)) continue;
             const int L1 = L0 | (1 << a);
             for (int j = 0; j < kWaveRegs; j++) {
-                if (((unsigned)j & w.cReg) != w.cReg) continue;
+                if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
                 const real r0 = vr[L0][j], i0 = vi[L0][j], r1 = vr[L1][j], i1 = vi[L1][j];
                 real *R0 = &vr[L0][j], *I0 = &vi[L0][j], *R1 = &vr[L1][j], *I1 = &vi[L1][j];
                 switch (kind) {
@@ -382,7 +382,7 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         return;
     }
     for (int lane = 0; lane < kVLanes; lane++) {
-        if (((unsigned)lane & w.cLane) != w.cLane) continue;
+        if ((((unsigned)lane ^ w.fLane) & w.cLane) != w.cLane) continue;
         if ((unsigned)lane & w.cLaneZero) continue;
         real* r = vr[lane];
         real* i = vi[lane];
@@ -405,7 +405,7 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         }
         if (kind >= WKind::DROT && kind <= WKind::DROTN) {
             for (int j = 0; j < kWaveRegs; j++) {
-                if (((unsigned)j & w.cReg) != w.cReg) continue;
+                if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
                 real &x = r[j], &y = i[j];
                 if (kind == WKind::DNEG || kind == WKind::DROTN) x = -x, y = -y;
                 if (kind == WKind::DROT || kind == WKind::DROTN) rot(x, y, false);
@@ -423,7 +423,7 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         }
         if (kind == WKind::DIAG || kind == WKind::D2S || kind == WKind::D2L) {
             for (int j = 0; j < kWaveRegs; j++) {
-                if (((unsigned)j & w.cReg) != w.cReg) continue;
+                if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
                 real tr = m[0], ti = m[1];
                 if (kind == WKind::D2S && ((j >> w.a) & 1)) tr = m[2], ti = m[3];
                 if (kind == WKind::D2L && ((lane >> w.a) & 1)) tr = m[2], ti = m[3];
@@ -436,7 +436,7 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
         const int a = w.a;
         for (int j = 0; j < kWaveRegs; j++) {
             if ((j >> a) & 1) continue;
-            if (((unsigned)j & w.cReg) != w.cReg) continue;
+            if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
             const int f = j | (1 << a);
             const real r0 = r[j], i0 = i[j], r1 = r[f], i1 = i[f];
             switch (kind) {
@@ -575,7 +575,9 @@ void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePas
     for (int lane = 0; lane < kVLanes; lane++)
         for (int j = 0; j < kWaveRegs; j++) {
             ld[lane][j] = offsetOf(ps.pos, ps.ldSlot, ps.ldLane, lane, j);
-            st[lane][j] = offsetOf(ps.stPos, ps.stSlot, ps.stLane, lane, j);   // relabelling passes store permuted
+            // relabelling passes store permuted; pending exchanges (stFlip)
+            // store register j where its partner belongs
+            st[lane][j] = offsetOf(ps.stPos, ps.stSlot, ps.stLane, lane ^ (int)ps.stFlipLane, j ^ (int)ps.stFlip);
         }
     dumpWavePass(wp, ps);
     TilePass tp;

@@ -324,14 +324,16 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     want = SCENARIOS[name](genv)
     out = str(tmp_path / f"{name}_{ranks}.npz")
     extra = {"QUEST_BACKEND": "hip", "QUEST_COMM": transport.split("-")[0], "PYTHONPATH": os.path.dirname(here),
-             "QUEST_COMM_TIMEOUT": "100"}
+             "QUEST_COMM_TIMEOUT": "180"}
     if transport == "ipc-nopipe":
         extra["QUEST_EXCHANGE_PIPELINE"] = "0"
     if slice_kb:
         extra["QUEST_EXCHANGE_SLICE_KB"] = slice_kb
-    res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks, env_extra=extra, timeout=110)
-    for r, p in enumerate(res):
-        assert p.returncode == 0, f"rank {r}:\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
+    res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks, env_extra=extra, timeout=200)
+    # every rank's output on failure: the first rank's error is often only
+    # "peer closed the connection" from another rank that failed first
+    bad = [(r, p) for r, p in enumerate(res) if p.returncode != 0]
+    assert not bad, "\n".join(f"rank {r} (rc {p.returncode}):\n{p.stdout[-1500:]}\n{p.stderr[-2500:]}" for r, p in bad)
     with np.load(out, allow_pickle=False) as z:
         got = {k: z[k] for k in z.files}
     assert int(got["_ranks"]) == ranks

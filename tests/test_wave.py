@@ -109,3 +109,56 @@ def test_wave_kernel_matches_lds_kernel_gpu(env):
         reg.close()
     capi.setQuESTTuning("tile_mode", 3)
     assert np.max(np.abs(outs[0] - outs[3])) < 1e-12
+
+
+XFRAME = r'''
+import os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import quest_amd as qa
+from helpers import GATES_1Q, GATES_2Q, GATES_MQ, apply_named, oracle_for, random_qubits
+
+env = qa.Env()
+n = 16
+rng = np.random.default_rng(int(sys.argv[2]))
+r = qa.Register(env, n)
+o = oracle_for(r, rng)
+names = GATES_1Q + GATES_2Q + GATES_MQ
+for step in range(300):
+    # an X, then gates that may use its qubit as target, control or phase mask
+    q = int(rng.integers(n))
+    apply_named(r, o, "x", [q], rng)
+    for _ in range(int(rng.integers(1, 4))):
+        name = names[rng.integers(len(names))]
+        k = 1 if name in GATES_1Q else 2 if name in GATES_2Q else int(rng.integers(2, 5))
+        qs = random_qubits(rng, n, k)
+        if rng.random() < 0.6 and q not in qs:
+            qs[int(rng.integers(k))] = q
+        apply_named(r, o, name, qs, rng)
+err = np.max(np.abs(r.to_numpy() - o.v))
+print("xframe err", err)
+assert err < 1e-10, err
+'''
+
+
+@pytest.mark.parametrize("frame", ["1", "0"])
+def test_exchange_frame_emulated_on_host(frame):
+    """Deferred X gates (planWavePass exchange frame): X on random qubits
+    followed by gates that use that qubit as target, control (register, lane
+    and wave bits) or phase mask, on the wave planner's host emulation,
+    against the NumPy oracle; QUEST_WAVE_XFRAME=0 executes every X."""
+    for seed in (1, 2):
+        out = _run(["-c", XFRAME, ROOT, str(seed)],
+                   {"QUEST_BACKEND": "cpu", "QUEST_CPU_PLANNER": "3", "QUEST_WAVE_XFRAME": frame})
+        assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+        assert "xframe err" in out.stdout
+
+
+@pytest.mark.gpu
+def test_exchange_frame_gpu():
+    """The exchange-frame stress on the GPU kernel (20 qubits: wave passes),
+    against the NumPy oracle."""
+    script = XFRAME.replace("n = 16", "n = 20")
+    out = _run(["-c", script, ROOT, "3"], {"QUEST_BACKEND": "hip"}, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "xframe err" in out.stdout

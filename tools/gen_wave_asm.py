@@ -425,7 +425,8 @@ class Gen:
     # the host-computed mask of the registers that pass, bit j) ----
     def ctrl_begin(self):
         # LM (s[96:97]) = lanes with (lane & cLane) == cLane
-        self.e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
+        self.e(f"v_xor_b32_e32 v{self.vTmp}, s71, v{self.vLane}")   # aux: lane bits the planner flipped
+        self.e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vTmp}")
         self.e(f"v_cmp_eq_u32_e64 s[96:97], s70, v{self.vTmp}")
         self.e("s_nop 4")
         self.e("s_mov_b64 exec, s[96:97]")
@@ -655,7 +656,8 @@ class Gen:
         self.handler(idx_ph(kind, creg, lane), f"{kind}_m{creg}_l{lane}")
         e = self.e
         if lane:
-            e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
+            e(f"v_xor_b32_e32 v{self.vTmp}, s71, v{self.vLane}")
+            e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vTmp}")
             e(f"v_cmp_eq_u32_e64 s[96:97], s70, v{self.vTmp}")
             e("s_nop 4")
             e("s_mov_b64 exec, s[96:97]")
@@ -727,8 +729,8 @@ class Gen:
 
     def gen_d2l(self, ctrl):
         self.handler(idx_d2l(ctrl), f"D2L_c{ctrl}")
-        # per-lane coefficient: lane bit aux (s71) ? d1 : d0
-        self.e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, s71, 1")
+        # per-lane coefficient: lane bit m[4] (its low dword) ? d1 : d0
+        self.e(f"v_bfe_u32 v{self.vTmp}, v{self.vLane}, s{76 + 4 * self.P}, 1")
         self.e(f"v_cmp_ne_u32_e64 {SEL}, 0, v{self.vTmp}")
         C0, C1, T0, T1 = self.C0, self.C1, self.T[14], self.T[15]
         self.e(f"{self.MOV} {self.vp(C0)}, {self.sm(0)}")
@@ -771,7 +773,8 @@ class Gen:
             self.back()
             return
         C0, C1 = self.C0, self.C1
-        e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vLane}")
+        e(f"v_xor_b32_e32 v{self.vTmp}, s71, v{self.vLane}")
+        e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vTmp}")
         e(f"v_cmp_eq_u32_e64 {SEL}, s70, v{self.vTmp}")
         e(f"{self.MOV} {self.vp(C0)}, {self.sm(0)}")
         e(f"{self.MOV} {self.vp(C1)}, {self.sm(1)}")
