@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 
 #include "router.hpp"
 
@@ -425,7 +426,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             }
         }
     };
-    auto emit = [&](WaveOp w) {
+    std::function<void(WaveOp)> emit = [&](WaveOp w) {
         const bool free = w.cReg == 0 && w.cLane == 0 && w.cLaneZero == 0 && w.ctrlOut == 0;
         if (frameOn && free && w.kind == (int)WKind::SWAP && w.a >= VB) {
             F ^= 1u << lay.slotBit[w.a];
@@ -433,6 +434,25 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         }
         if (frameOn && free && w.kind == (int)WKind::LSWAP) {
             F ^= 1u << lay.laneBit[w.a];
+            return;
+        }
+        // Y = i X Z (-Y = -i X Z): a sign flip on the bit's 1 half, the X into
+        // the frame, the i to the pass's owed factor
+        const bool laneY = w.kind == (int)WKind::LANTI && w.m[0] == 0 && w.m[2] == 0 && std::fabs(w.m[1]) == 1 &&
+                           w.m[3] == -w.m[1];
+        if (frameOn && free && (((w.kind == (int)WKind::YSW || w.kind == (int)WKind::YSWC) && w.a >= VB) || laneY)) {
+            // YSW is Y, YSWC -Y; a lane Y has m01 = -i (m[1] = -1)
+            const bool minus = laneY ? w.m[1] > 0 : w.kind == (int)WKind::YSWC;
+            WaveOp z = blank((int)WKind::DNEG);
+            if (laneY)
+                z.cLane = 1u << w.a;
+            else
+                z.cReg = 1u << w.a;
+            emit(z);
+            WaveOp x = blank(laneY ? (int)WKind::LSWAP : (int)WKind::SWAP);
+            x.a = w.a;
+            emit(x);
+            sig.mul(0, minus ? -1 : 1);
             return;
         }
         if (!F) {
