@@ -10,6 +10,8 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../hip/qa_hip.h"
 
 namespace qa {
@@ -108,7 +110,28 @@ char* importBuffer(int peer, const Token& t) {
         g_imported.erase(g_imported.begin() + (long)lru);
     }
     void* ptr = nullptr;
-    QA_HIP_CHECK(hipIpcOpenMemHandle(&ptr, t.handle, hipIpcMemLazyEnablePeerAccess));
+    // Several processes mapping each other's buffers on one device: the
+    // driver has been seen to refuse an open with "invalid device pointer"
+    // now and then (4 ranks, dmabuf IPC).  Drain, unmap this peer's other
+    // buffers and try again a few times before giving up.
+    hipError_t rc = hipIpcOpenMemHandle(&ptr, t.handle, hipIpcMemLazyEnablePeerAccess);
+    for (int attempt = 1; rc != hipSuccess && attempt <= 3; attempt++) {
+        (void)hipGetLastError();
+        QA_HIP_CHECK(hipDeviceSynchronize());
+        for (size_t i = 0; i < g_imported.size();) {
+            if (g_imported[i].peer == peer) {
+                (void)hipIpcCloseMemHandle(g_imported[i].ptr);
+                g_imported.erase(g_imported.begin() + (long)i);
+            } else {
+                i++;
+            }
+        }
+        usleep(2000u * (unsigned)attempt);
+        fprintf(stderr, "QuEST ipc: rank %d: opening rank %d's buffer %llu failed (%s), retry %d\n", g_rank, peer,
+                t.id, hipGetErrorString(rc), attempt);
+        rc = hipIpcOpenMemHandle(&ptr, t.handle, hipIpcMemLazyEnablePeerAccess);
+    }
+    QA_HIP_CHECK(rc);
     g_imported.push_back({peer, t.id, static_cast<char*>(ptr), g_clock});
     return static_cast<char*>(ptr);
 }
