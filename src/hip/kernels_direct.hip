@@ -11,6 +11,8 @@
 // array, all loads issued before the first use.
 #include "qa_hip.h"
 
+#include <type_traits>
+
 namespace qa {
 namespace hipk {
 
@@ -48,13 +50,17 @@ __device__ __forceinline__ void mat2apply(const Cm2<T>& m, T& r0, T& i0, T& r1, 
     i1 = m.r[2] * b + m.i[2] * a + m.r[3] * d + m.i[3] * c;
 }
 
-// This thread's groups of UNR units: u0 + k * step, k < UNR.  BLK = false:
+// This thread's groups of UNR units: u0 + k * step, k < UNR.  MODE 0:
 // grid-stride (consecutive groups of one thread lie a whole grid apart);
-// BLK = true: each workgroup owns a contiguous run of 256 * UNR units, so
-// the UNR loads of a wave are 4 KiB apart instead of a grid's worth.
-template <bool BLK, int UNR, typename F>
+// MODE 1: each workgroup owns contiguous runs of 256 * UNR units, so the UNR
+// loads of a wave are 4 KiB apart instead of a grid's worth; MODE 2: as 1
+// with exactly one run per workgroup and units a multiple of the run (no
+// bounds checks: every load is unconditional and issued back to back).
+template <int MODE, int UNR, typename F>
 __device__ __forceinline__ void forUnits(long long units, F&& f) {
-    if constexpr (BLK) {
+    if constexpr (MODE == 2) {
+        f((long long)blockIdx.x * blockDim.x * UNR + threadIdx.x, (long long)blockDim.x);
+    } else if constexpr (MODE == 1) {
         const long long per = (long long)blockDim.x * UNR;
         for (long long c = blockIdx.x; c * per < units; c += gridDim.x) f(c * per + threadIdx.x, (long long)blockDim.x);
     } else {
@@ -66,20 +72,20 @@ __device__ __forceinline__ void forUnits(long long units, F&& f) {
 
 // target >= log2(VN): a vector at `up` (target bit 0) pairs with the vector
 // at up + 2^t.
-template <typename T, bool BLK>
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                         InsertBits ib, long long tbit, Cm2<T> m) {
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::n;
-    constexpr int UNR = 2;
-    forUnits<BLK, UNR>(units, [&](long long u0, long long step) {
+    constexpr int UNR = 4;  // tools/stream_variants.hip: 4 pairs per thread 1-4 % faster than 2
+    forUnits<MODE, UNR>(units, [&](long long u0, long long step) {
         long long up[UNR];
         V ar[UNR], ai[UNR], br[UNR], bi[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
             const long long u = u0 + k * step;
-            up[k] = u < units ? insertAll(u * VN, ib) : -1;
-            if (up[k] >= 0) {
+            up[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
+            if (MODE == 2 || up[k] >= 0) {
                 ar[k] = streamLoad(reinterpret_cast<const V*>(re + up[k]));
                 ai[k] = streamLoad(reinterpret_cast<const V*>(im + up[k]));
                 br[k] = streamLoad(reinterpret_cast<const V*>(re + up[k] + tbit));
@@ -88,7 +94,7 @@ __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* _
         }
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
-            if (up[k] < 0) continue;
+            if (MODE != 2 && up[k] < 0) continue;
             T* pr = reinterpret_cast<T*>(&ar[k]);
             T* pi = reinterpret_cast<T*>(&ai[k]);
             T* qr = reinterpret_cast<T*>(&br[k]);
@@ -107,35 +113,103 @@ __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* _
 }
 
 // target inside one vector (bit 0 for fp64, bits 0-1 for fp32)
-template <typename T, bool BLK>
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                      InsertBits ib, int t, Cm2<T> m) {
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::n;
     constexpr int UNR = 4;
-    forUnits<BLK, UNR>(units, [&](long long u0, long long step) {
+    forUnits<MODE, UNR>(units, [&](long long u0, long long step) {
         long long at[UNR];
         V vr[UNR], vi[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
             const long long u = u0 + k * step;
-            at[k] = u < units ? insertAll(u * VN, ib) : -1;
-            if (at[k] >= 0) {
+            at[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
+            if (MODE == 2 || at[k] >= 0) {
                 vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
                 vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
             }
         }
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
-            if (at[k] < 0) continue;
+            if (MODE != 2 && at[k] < 0) continue;
             T* pr = reinterpret_cast<T*>(&vr[k]);
             T* pi = reinterpret_cast<T*>(&vi[k]);
+            // element indices must be compile-time (a runtime-indexed
+            // register array goes to scratch: 7.7 instead of 5.9 ms per H)
+            auto pairs = [&](auto tc) {
+                constexpr int TT = decltype(tc)::value;
+#pragma unroll
+                for (int e = 0; e < VN; e++) {
+                    if (e & (1 << TT)) continue;
+                    if ((((unsigned)at[k] + e) & ib.predMask) != ib.predMask) continue;
+                            mat2apply(m, pr[e], pi[e], pr[e | (1 << TT)], pi[e | (1 << TT)]);
+                }
+            };
+            if (VN == 2 || t == 0)
+                pairs(std::integral_constant<int, 0>{});
+            else
+                pairs(std::integral_constant<int, 1>{});
+            streamStore(reinterpret_cast<V*>(re + at[k]), vr[k]);
+            streamStore(reinterpret_cast<V*>(im + at[k]), vi[k]);
+        }
+    });
+}
+
+// target inside the 128-byte line but above one vector (fp64 bits 1-3,
+// fp32 bits 2-4): every lane loads ONE contiguous vector per array (the
+// access pattern of the in-vector kernel: 1 KiB per wave instruction), gets
+// its partner's vector -- lane ^ 2^(t - vbits), the same line -- by a lane
+// shuffle and computes its own half of the pair.  The pair kernel above
+// would load two half-used 2 KiB spans per instruction instead (10.5 ms per
+// H at 30 qubits against 7.3 in-vector, tools/direct_ab.py).  Controls
+// below the line are per-element predicates; both halves of a pair agree on
+// them, so a lane that fails keeps its amplitudes.
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void mat2ShflKernel(T* __restrict__ re, T* __restrict__ im, long long units,
+                                                      InsertBits ib, int t, int lx, Cm2<T> m) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = Vec16<T>::n;
+    constexpr int UNR = 4;
+    forUnits<MODE, UNR>(units, [&](long long u0, long long step) {
+        long long at[UNR];
+        V vr[UNR], vi[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; k++) {
+            const long long u = u0 + k * step;
+            // out-of-range lanes still take part in the shuffles (whole
+            // 8-lane partner groups are in or out together)
+            at[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
+            if (MODE == 2 || at[k] >= 0) {
+                vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
+                vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
+            } else {
+                vr[k] = V{};
+                vi[k] = V{};
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < UNR; k++) {
+            T* pr = reinterpret_cast<T*>(&vr[k]);
+            T* pi = reinterpret_cast<T*>(&vi[k]);
+            T qr[VN], qi[VN];
 #pragma unroll
             for (int e = 0; e < VN; e++) {
-                if (e & (1 << t)) continue;
+                qr[e] = __shfl_xor(pr[e], lx);
+                qi[e] = __shfl_xor(pi[e], lx);
+            }
+            if (MODE != 2 && at[k] < 0) continue;
+            const bool hi = ((at[k] >> t) & 1) != 0;
+            // own amplitude a (row `hi` of the matrix), partner b
+            const T ar = hi ? m.r[3] : m.r[0], ai = hi ? m.i[3] : m.i[0];
+            const T br = hi ? m.r[2] : m.r[1], bi = hi ? m.i[2] : m.i[1];
+#pragma unroll
+            for (int e = 0; e < VN; e++) {
                 if ((((unsigned)at[k] + e) & ib.predMask) != ib.predMask) continue;
-                const int f = e | (1 << t);
-                mat2apply(m, pr[e], pi[e], pr[f], pi[f]);
+                const T x = pr[e], y = pi[e];
+                pr[e] = ar * x - ai * y + br * qr[e] - bi * qi[e];
+                pi[e] = ar * y + ai * x + br * qi[e] + bi * qr[e];
             }
             streamStore(reinterpret_cast<V*>(re + at[k]), vr[k]);
             streamStore(reinterpret_cast<V*>(im + at[k]), vi[k]);
@@ -144,27 +218,27 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
 }
 
 // multiply the amplitudes whose mask bits are all 1
-template <typename T, bool BLK>
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                         InsertBits ib, T tr, T ti) {
     using V = typename Vec16<T>::type;
     constexpr int VN = Vec16<T>::n;
     constexpr int UNR = 4;
-    forUnits<BLK, UNR>(units, [&](long long u0, long long step) {
+    forUnits<MODE, UNR>(units, [&](long long u0, long long step) {
         long long at[UNR];
         V vr[UNR], vi[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
             const long long u = u0 + k * step;
-            at[k] = u < units ? insertAll(u * VN, ib) : -1;
-            if (at[k] >= 0) {
+            at[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
+            if (MODE == 2 || at[k] >= 0) {
                 vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
                 vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
             }
         }
 #pragma unroll
         for (int k = 0; k < UNR; k++) {
-            if (at[k] < 0) continue;
+            if (MODE != 2 && at[k] < 0) continue;
             T* pr = reinterpret_cast<T*>(&vr[k]);
             T* pi = reinterpret_cast<T*>(&vi[k]);
 #pragma unroll
@@ -180,14 +254,41 @@ __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* _
     });
 }
 
-int directGrid(long long units) {
-    long long g = (units + 255) / 256;
-    const long long mx = (long long)numCUs() * 16;
-    if (g > mx) g = mx;
+// directLayout 2 (default): one run of 256 * UNR units per workgroup and
+// as many workgroups as runs -- no loop, the dispatcher keeps every CU fed
+// (tools/stream_variants.hip: 5.28 ms per H at 30 qubits, 6.5 TB/s, against
+// 5.40 ms with 16 looping workgroups per CU on the same box; in the library
+// 6.15-6.38 vs 6.65-7.12 ms on a slower box, tools/direct_ab.py).  1: at
+// most 16 workgroups per CU, each looping over runs; 0: grid-stride units.
+int directMode(long long units, int unr) {
+    const int lay = tuning().directLayout;
+    if (lay >= 2) return units % (256ll * unr) == 0 ? 2 : 1;
+    return lay;
+}
+
+int directGrid(long long units, int unr) {
+    const long long per = 256ll * (tuning().directLayout >= 2 ? unr : 1);
+    long long g = (units + per - 1) / per;
+    if (tuning().directLayout < 2) {
+        const long long mx = (long long)numCUs() * 16;
+        if (g > mx) g = mx;
+    }
+    if (g > 0x7fffffffll) g = 0x7fffffffll;
     return (int)(g < 1 ? 1 : g);
 }
 
 }  // namespace
+
+#define QA_DIRECT_LAUNCH(KER, UNR, ...)                                                                          \
+    do {                                                                                                      \
+        const dim3 grid_(directGrid(units, UNR));                                                              \
+        switch (directMode(units, UNR)) {                                                                      \
+            case 2: hipLaunchKernelGGL((KER<real, 2>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;     \
+            case 1: hipLaunchKernelGGL((KER<real, 1>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;     \
+            default: hipLaunchKernelGGL((KER<real, 0>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;    \
+        }                                                                                                      \
+        QA_HIP_CHECK(hipGetLastError());                                                                       \
+    } while (0)
 
 bool launchDirectOp(real* re, real* im, int L, const Op& op) {
     constexpr int VN = Vec16<real>::n;
@@ -196,10 +297,8 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
     const long long N = 1ll << L;
     if (N < (long long)VN * 2048) return false;  // small states: one tile pass is as good
     if (op.kind != OpKind::Mat2 && op.kind != OpKind::Diag) return false;
-    const bool blk = tuning().directLayout == 1;
-    // Targets / masks inside a 128-byte line: the LDS tile pass streams
-    // faster than the in-register pair kernels (measured 6.7 vs 7.3-8.9 ms
-    // per H on 30 qubits, tools/layout_probe.py), so leave those to it.
+    // directLowToTile = 1: targets / controls inside a 128-byte line go to
+    // the LDS tile pass instead of the in-vector and lane-shuffle kernels.
     if (tuning().directLowToTile) {
         if (op.kind == OpKind::Mat2 && op.t[0] < LINE) return false;
         if ((op.ctrl & ((1ull << LINE) - 1)) != 0) return false;
@@ -225,13 +324,7 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
         if (ni > 8) return false;
         for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
         const long long units = (N >> ni) / VN;
-        if (blk)
-            hipLaunchKernelGGL((diagDirectKernel<real, true>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
-                               units, ib, op.m[0].re, op.m[0].im);
-        else
-            hipLaunchKernelGGL((diagDirectKernel<real, false>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
-                               units, ib, op.m[0].re, op.m[0].im);
-        QA_HIP_CHECK(hipGetLastError());
+        QA_DIRECT_LAUNCH(diagDirectKernel, 4, re, im, units, ib, op.m[0].re, op.m[0].im);
         return true;
     }
 
@@ -241,7 +334,7 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
         m.r[i] = op.m[i].re;
         m.i[i] = op.m[i].im;
     }
-    if (t >= vbits) {
+    if (t >= LINE) {
         if (ni > 7) return false;
         // insert the target among the (ascending) high controls
         int all[9], na = 0;
@@ -256,24 +349,18 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
         if (!placed) all[na++] = t;
         for (int i = 0; i < na; i++) ib.pos[ib.n++] = all[i];
         const long long units = (N >> na) / VN;
-        if (blk)
-            hipLaunchKernelGGL((mat2DirectKernel<real, true>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
-                               units, ib, 1ll << t, m);
-        else
-            hipLaunchKernelGGL((mat2DirectKernel<real, false>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
-                               units, ib, 1ll << t, m);
+        QA_DIRECT_LAUNCH(mat2DirectKernel, 4, re, im, units, ib, 1ll << t, m);
+    } else if (t >= vbits) {
+        if (ni > 8) return false;
+        for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
+        const long long units = (N >> ni) / VN;
+        QA_DIRECT_LAUNCH(mat2ShflKernel, 4, re, im, units, ib, t, 1 << (t - vbits), m);
     } else {
         if (ni > 8) return false;
         for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
         const long long units = (N >> ni) / VN;
-        if (blk)
-            hipLaunchKernelGGL((mat2LowKernel<real, true>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
-                               units, ib, t, m);
-        else
-            hipLaunchKernelGGL((mat2LowKernel<real, false>), dim3(directGrid(units)), dim3(256), 0, stream(), re, im,
-                               units, ib, t, m);
+        QA_DIRECT_LAUNCH(mat2LowKernel, 4, re, im, units, ib, t, m);
     }
-    QA_HIP_CHECK(hipGetLastError());
     return true;
 }
 

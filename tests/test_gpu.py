@@ -374,7 +374,7 @@ def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
     r.close()
 
 
-@pytest.mark.parametrize("layout", [0, 1])
+@pytest.mark.parametrize("layout", [0, 1, 2])
 @pytest.mark.parametrize("low_to_tile", [0, 1])
 def test_direct_kernel_variants(genv, layout, low_to_tile):
     """Unfused gates through every direct-kernel variant (unit order, low
@@ -397,6 +397,40 @@ def test_direct_kernel_variants(genv, layout, low_to_tile):
         o.apply(np.diag([1, np.exp(1j * np.pi / 4)]), t)
     assert_close(reg, o)
     reg.close()
+
+
+def test_direct_kernel_variants_fp32():
+    """The fp32 unfused kernels (in-vector targets 0-1, lane-shuffle targets
+    2-4, pair kernel above the line) under both launch layouts, 16 qubits, vs
+    the oracle -- subprocess bound to the fp32 HIP library."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path.insert(0, 'tests')\n"
+        "import numpy as np, quest_amd as qa\n"
+        "from helpers import apply_random_ops, oracle_for, state_of\n"
+        "from quest_amd.ops import capi\n"
+        "assert capi.getQuEST_PREC() == 1\n"
+        "e = qa.Env(); capi.setGateFusion(0)\n"
+        "for lay in (1, 2):\n"
+        "    for low in (0, 1):\n"
+        "        capi.setQuESTTuning('direct_layout', lay); capi.setQuESTTuning('direct_low_to_tile', low)\n"
+        "        rng = np.random.default_rng(lay * 10 + low)\n"
+        "        r = qa.Register(e, 16); o = oracle_for(r, rng)\n"
+        "        apply_random_ops(r, o, rng, 80)\n"
+        "        for t in range(16):\n"
+        "            r.h(t); o.apply(np.array([[1, 1], [1, -1]]) / np.sqrt(2), t)\n"
+        "            r.t(t); o.apply(np.diag([1, np.exp(1j * np.pi / 4)]), t)\n"
+        "        err = np.max(np.abs(state_of(r) - o.v)); r.close()\n"
+        "        assert err < 2e-5, (lay, low, err)\n"
+        "print('fp32 direct ok')\n"
+    )
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, QUEST_BACKEND="hip", QUEST_PREC="1"))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "fp32 direct ok" in out.stdout
 
 
 def test_tile_qubits_12_matches_oracle(genv):
