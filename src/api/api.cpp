@@ -933,6 +933,10 @@ int setQuESTTuning(const char* key, int value) {
         rt().verify = value != 0;
         return 1;
     }
+    if (key && !strcmp(key, "plan_max_ops")) {
+        planMaxOps() = value;
+        return 1;
+    }
     if (key && !strcmp(key, "wave_relabel")) {
         waveRelabel() = value != 0;
         return 1;
@@ -951,6 +955,8 @@ int getQuESTTuning(const char* key, int* value) {
         v = fuseBlocks() ? 1 : 0;
     else if (key && !strcmp(key, "verify"))
         v = rt().verify ? 1 : 0;
+    else if (key && !strcmp(key, "plan_max_ops"))
+        v = planMaxOps();
     else if (key && !strcmp(key, "wave_relabel"))
         v = waveRelabel() ? 1 : 0;
     else

@@ -265,6 +265,14 @@ bool& fuseBlocks() {
     return on;
 }
 
+int& planMaxOps() {
+    static int m = [] {
+        const char* e = getenv("QUEST_PLAN_MAX_OPS");
+        return e ? atoi(e) : 0;
+    }();
+    return m;
+}
+
 int& fuseBlockQubits() {
     static int q = 2;
     return q;
@@ -505,6 +513,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
     std::vector<char> done(n, 0);
     int first = 0;
     std::vector<int> take, best;
+    const int maxOps = planMaxOps();
     // one greedy scan from `first` with the high bits `preset` claimed up front
     auto scan = [&](u64 preset, std::vector<int>& picked) {
         picked.clear();
@@ -517,7 +526,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             const u64 touch = tg | ops[i].ctrl;
             const bool free = !(tg & blockedTouch) && !(touch & blockedTg);
             const u64 need = high | (tg & ~low);
-            if (free && popcount64(need) <= highSlots) {
+            if (free && popcount64(need) <= highSlots && (maxOps <= 0 || (int)picked.size() < maxOps)) {
                 high = need;
                 picked.push_back(i);
             } else {

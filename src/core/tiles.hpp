@@ -129,6 +129,11 @@ bool& fuseBlocks();
 // Largest block fuseGates forms: 2 (4x4 blocks, default) or 1 (runs of
 // one-qubit gates only; the wave engine keeps CNOTs and controls apart)
 int& fuseBlockQubits();
+// Most ops one fused pass takes (0: no limit; env QUEST_PLAN_MAX_OPS,
+// setQuESTTuning "plan_max_ops").  A pass whose ops cost more VALU time than
+// its HBM stream is compute-bound while the passes after it wait on memory;
+// a cap moves the surplus into them.
+int& planMaxOps();
 
 // Split `ops` (physical local positions, L local qubits) into passes of at
 // most kmax tile qubits (kmax >= cmin + 4).  With fuse=true ops are reordered
