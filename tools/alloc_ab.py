@@ -18,6 +18,9 @@ G = 1 << 30
 # (label, QUEST_ALLOC_MODE, QUEST_IM_OFFSET, QUEST_ALLOC_PAD) -- sizes for 30 qubits (8 GiB arrays)
 PLACEMENTS = [("split (default) #1", 0, 0, 0), ("contiguous #1", 2, 0, 0), ("split (default) #2", 0, 0, 0),
               ("contiguous #2", 2, 0, 0), ("split (default) #3", 0, 0, 0), ("contiguous #3", 2, 0, 0)]
+if os.environ.get("ALLOC_AB_SET") == "distance":
+    # joint allocations, im starting D after re (D = 8 GiB + QUEST_IM_OFFSET)
+    PLACEMENTS = [(f"joint, im {8 + o} GiB after re", 1, o * G, 0) for o in (0, 4, 8, 12, 24, 0, 8)]
 if os.environ.get("ALLOC_AB_SET") == "offsets":
     PLACEMENTS = [("split (default)", 0, 0, 0), ("joint, im 24 GiB after re", 1, 24 * G, 0),
                   ("split, each in a 32 GiB alloc", 0, 0, 24 * G), ("joint in a 48 GiB alloc", 1, 0, 32 * G),
