@@ -780,6 +780,11 @@ void addDensityMatrix(Qureg combineQureg, qreal otherProb, Qureg otherQureg) {
 // decoherence
 // ===========================================================================
 
+// Dephasing strengths whose factor is at least this large run as diagonal
+// ops (their inverse powers stay well inside the range of qreal); stronger
+// dephasing keeps the channel form.
+constexpr double kDiagDephaseMin = 1e-3;
+
 void applyOneQubitDephaseError(Qureg qureg, const int targetQubit, qreal prob) {
     if (!v::densMatr(qureg, __func__) || !v::target(qureg, targetQubit, __func__) ||
         !v::oneQubitDephaseProb(prob, __func__))
@@ -787,8 +792,20 @@ void applyOneQubitDephaseError(Qureg qureg, const int targetQubit, qreal prob) {
     real dephase = 2 * prob;
     if (dephase == 0) return;
     real f = 1 - dephase;
+    QuregImpl& q = Q(qureg);
+    if (std::fabs(f) >= kDiagDephaseMin) {
+        // f on the elements whose row and column bits differ, as three
+        // diagonal ops (factors on all-ones masks: f^r f^c f^(-2rc)); they
+        // need no tile bits, so they fuse into any pass instead of forming a
+        // (row, column) channel that needs both bits in one tile
+        const int r = targetQubit, c = targetQubit + q.nRep, rc[2] = {r, c};
+        router::diag(q, &r, 1, {f, 0});
+        router::diag(q, &c, 1, {f, 0});
+        router::diag(q, rc, 2, {1 / (f * f), 0});
+        return;
+    }
     const real m[16] = {1, 0, 0, 0, 0, f, 0, 0, 0, 0, f, 0, 0, 0, 0, 1};
-    realMat4(Q(qureg), targetQubit, m);
+    realMat4(q, targetQubit, m);
 }
 
 void applyTwoQubitDephaseError(Qureg qureg, int qubit1, int qubit2, qreal prob) {
@@ -799,6 +816,24 @@ void applyTwoQubitDephaseError(Qureg qureg, int qubit1, int qubit2, qreal prob) 
     real d = (4 * prob) / 3.0;
     if (d == 0) return;
     QuregImpl& q = Q(qureg);
+    const real g = 1 - d;
+    if (std::fabs(g) >= kDiagDephaseMin) {
+        // g on the elements with (r1, r2) != (c1, c2): g^(1 - [r1==c1][r2==c2])
+        // expanded over the bits into factors g^e on all-ones masks (15
+        // diagonal ops that fuse into any pass, as for one qubit)
+        const int r1 = qubit1, r2 = qubit2, c1 = qubit1 + q.nRep, c2 = qubit2 + q.nRep;
+        struct Term {
+            int n, e;
+            int b[4];
+        };
+        const Term terms[15] = {{1, 1, {r1}},           {1, 1, {c1}},           {2, -2, {r1, c1}},
+                                {1, 1, {r2}},           {1, 1, {c2}},           {2, -2, {r2, c2}},
+                                {2, -1, {r1, r2}},      {2, -1, {r1, c2}},      {2, -1, {c1, r2}},
+                                {2, -1, {c1, c2}},      {3, 2, {r1, r2, c2}},   {3, 2, {c1, r2, c2}},
+                                {3, 2, {r1, c1, r2}},   {3, 2, {r1, c1, c2}},   {4, -4, {r1, c1, r2, c2}}};
+        for (const Term& t : terms) router::diag(q, t.b, t.n, {(real)std::pow((double)g, t.e), 0});
+        return;
+    }
     router::densChan2(q, qubit1, qubit2, qubit1 + q.nRep, qubit2 + q.nRep, 1 - d, 1, 0);
 }
 

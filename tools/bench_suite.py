@@ -195,6 +195,17 @@ def run_density17(env, res, n=17):
         d.damping(q, 0.1)
     d.sync()
     t_damp = (time.perf_counter() - t0) / n
+    # dephasing (diagonal ops: they fuse into one pass) and two-qubit dephasing
+    t0 = time.perf_counter()
+    for q in range(n):
+        d.dephase(q, 0.1)
+    d.sync()
+    t_deph = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    for q in range(0, n - 1, 2):
+        d.dephase2(q, q + 1, 0.1)
+    d.sync()
+    t_deph2 = (time.perf_counter() - t0) / len(range(0, n - 1, 2))
     t0 = time.perf_counter()
     for q in range(n):
         d.h(q)
@@ -216,8 +227,10 @@ def run_density17(env, res, n=17):
     d.sync()
     t_layered = (time.perf_counter() - t0) / len(c.gates)
     res["density17"] = {"qubits": n, "amps": 1 << (2 * n), "damping_s_per_channel": t_damp,
+                        "dephase_s_per_channel": t_deph, "dephase2_s_per_channel": t_deph2,
                         "gate_s": t_gate, "layered_s_per_gate": t_layered, "trace": tr, "purity": pur}
-    print(f"density{n}: damping {1e3 * t_damp:.2f} ms/channel, gates {1e3 * t_gate:.2f} ms/gate (one layer), "
+    print(f"density{n}: damping {1e3 * t_damp:.2f} ms/channel, dephasing {1e3 * t_deph:.2f}, two-qubit "
+          f"dephasing {1e3 * t_deph2:.2f} ms/channel, gates {1e3 * t_gate:.2f} ms/gate (one layer), "
           f"layered {1e3 * t_layered:.2f} ms/gate (6 layers), trace {tr:.12f}, purity {pur:.6f}", flush=True)
     d.close()
 
