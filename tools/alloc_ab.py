@@ -19,8 +19,11 @@ G = 1 << 30
 PLACEMENTS = [("split (default) #1", 0, 0, 0), ("contiguous #1", 2, 0, 0), ("split (default) #2", 0, 0, 0),
               ("contiguous #2", 2, 0, 0), ("split (default) #3", 0, 0, 0), ("contiguous #3", 2, 0, 0)]
 if os.environ.get("ALLOC_AB_SET") == "distance":
-    # joint allocations, im starting D after re (D = 8 GiB + QUEST_IM_OFFSET)
-    PLACEMENTS = [(f"joint, im {8 + o} GiB after re", 1, o * G, 0) for o in (0, 4, 8, 12, 24, 0, 8)]
+    # joint allocations, im starting D GiB after re (QUEST_IM_OFFSET = D - array size);
+    # ALLOC_AB_ARRAY_GIB = the array size (8 at 30 qubits), ALLOC_AB_D = the distances
+    _a = float(os.environ.get("ALLOC_AB_ARRAY_GIB", "8"))
+    _ds = [float(x) for x in os.environ.get("ALLOC_AB_D", "8,12,16,20,32,8,16").split(",")]
+    PLACEMENTS = [(f"joint, im {d:g} GiB after re", 1, int((d - _a) * G), 0) for d in _ds]
 if os.environ.get("ALLOC_AB_SET") == "offsets":
     PLACEMENTS = [("split (default)", 0, 0, 0), ("joint, im 24 GiB after re", 1, 24 * G, 0),
                   ("split, each in a 32 GiB alloc", 0, 0, 24 * G), ("joint in a 48 GiB alloc", 1, 0, 32 * G),
