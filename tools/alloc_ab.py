@@ -24,6 +24,13 @@ if os.environ.get("ALLOC_AB_SET") == "distance":
     _a = float(os.environ.get("ALLOC_AB_ARRAY_GIB", "8"))
     _ds = [float(x) for x in os.environ.get("ALLOC_AB_D", "8,12,16,20,32,8,16").split(",")]
     PLACEMENTS = [(f"joint, im {d:g} GiB after re", 1, int((d - _a) * G), 0) for d in _ds]
+if os.environ.get("ALLOC_AB_SET") == "vmm":
+    # mode 3: one reserved address range, physical memory mapped for re and
+    # im only, im QUEST_IM_DIST bytes after re (this set sizes for 30 qubits)
+    PLACEMENTS = [("split (default)", 0, 0, 0), ("joint, im 16 GiB after re", 1, 8 * G, 0),
+                  ("vmm, im 16 GiB after re", 3, 16 * G, 0), ("vmm, im 8 GiB after re", 3, 8 * G, 0),
+                  ("vmm, im 32 GiB after re", 3, 32 * G, 0), ("vmm, im 16 GiB after re #2", 3, 16 * G, 0),
+                  ("split (default) #2", 0, 0, 0)]
 if os.environ.get("ALLOC_AB_SET") == "offsets":
     PLACEMENTS = [("split (default)", 0, 0, 0), ("joint, im 24 GiB after re", 1, 24 * G, 0),
                   ("split, each in a 32 GiB alloc", 0, 0, 24 * G), ("joint in a 48 GiB alloc", 1, 0, 32 * G),
@@ -56,6 +63,7 @@ def main():
     for label, mode, off, pad in order:
         os.environ["QUEST_ALLOC_MODE"] = str(mode)
         os.environ["QUEST_IM_OFFSET"] = str(off)
+        os.environ["QUEST_IM_DIST"] = str(off)
         os.environ["QUEST_ALLOC_PAD"] = str(pad)
         r = qa.Register(env, n)
         r.init_plus()
