@@ -783,7 +783,12 @@ void addDensityMatrix(Qureg combineQureg, qreal otherProb, Qureg otherQureg) {
 // Dephasing strengths whose factor is at least this large run as diagonal
 // ops (their inverse powers stay well inside the range of qreal); stronger
 // dephasing keeps the channel form.
+// QUEST_DEPHASE_DIAG=0 keeps the channel forms (A/B).
 constexpr double kDiagDephaseMin = 1e-3;
+bool dephaseDiag() {
+    static const bool on = !getenv("QUEST_DEPHASE_DIAG") || atoi(getenv("QUEST_DEPHASE_DIAG")) != 0;
+    return on;
+}
 
 void applyOneQubitDephaseError(Qureg qureg, const int targetQubit, qreal prob) {
     if (!v::densMatr(qureg, __func__) || !v::target(qureg, targetQubit, __func__) ||
@@ -793,7 +798,7 @@ void applyOneQubitDephaseError(Qureg qureg, const int targetQubit, qreal prob) {
     if (dephase == 0) return;
     real f = 1 - dephase;
     QuregImpl& q = Q(qureg);
-    if (std::fabs(f) >= kDiagDephaseMin) {
+    if (dephaseDiag() && std::fabs(f) >= kDiagDephaseMin) {
         // f on the elements whose row and column bits differ, as three
         // diagonal ops (factors on all-ones masks: f^r f^c f^(-2rc)); they
         // need no tile bits, so they fuse into any pass instead of forming a
@@ -817,7 +822,7 @@ void applyTwoQubitDephaseError(Qureg qureg, int qubit1, int qubit2, qreal prob) 
     if (d == 0) return;
     QuregImpl& q = Q(qureg);
     const real g = 1 - d;
-    if (std::fabs(g) >= kDiagDephaseMin) {
+    if (dephaseDiag() && std::fabs(g) >= kDiagDephaseMin) {
         // g on the elements with (r1, r2) != (c1, c2): g^(1 - [r1==c1][r2==c2])
         // expanded over the bits into factors g^e on all-ones masks (15
         // diagonal ops that fuse into any pass, as for one qubit)
