@@ -125,3 +125,41 @@ def test_one_pass_marginals_26q(genv):
     want = np.array([float(p.sum(dim=tuple(n - 1 - k for k in range(n) if k != q))[0]) for q in range(n)])
     np.testing.assert_allclose(got, want, rtol=0, atol=1e-12)
     r.close()
+
+
+@pytest.mark.parametrize("mode", [None, "0", "1", "2", "3"])
+def test_register_placements_agree_27q(genv, mode, monkeypatch):
+    """Every placement of a register's arrays (default: one allocation with
+    an 8 GiB gap between re and im; 0 two allocations; 1 joint; 2 physically
+    contiguous; 3 reserved address range with mapped arrays) gives the same
+    state bit for bit on a 27-qubit circuit (1 GiB arrays: the default takes
+    its gap), including amplitude reads and writes and a clone."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+
+    if mode is None:
+        monkeypatch.delenv("QUEST_ALLOC_MODE", raising=False)
+    else:
+        monkeypatch.setenv("QUEST_ALLOC_MODE", mode)
+        monkeypatch.setenv("QUEST_IM_OFFSET", str(1 << 30))
+        monkeypatch.setenv("QUEST_IM_DIST", str(3 << 30))
+    n = 27
+    circ = random_layered(n, 3, seed=27)
+    r = qa.Register(genv, n)
+    monkeypatch.delenv("QUEST_ALLOC_MODE", raising=False)
+    ref = qa.Register(genv, n)          # default placement
+    for reg in (r, ref):
+        reg.init_plus()
+        circ.apply(reg)
+        reg.set_amps(np.array([0.25 + 0.5j, -0.125j]), start=5)
+        reg.h(0)
+    idx = [0, 1, 5, 6, 12345, (1 << n) - 1]
+    got = [r.amp(i) for i in idx]
+    want = [ref.amp(i) for i in idx]
+    assert got == want
+    assert 2 - 2 * r.inner(ref).real < 1e-13
+    c = qa.Register(genv, n)
+    c.clone_from(r)
+    assert c.amp(12345) == r.amp(12345)
+    for reg in (r, ref, c):
+        reg.close()
