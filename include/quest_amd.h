@@ -31,12 +31,23 @@ void setFusionMaxQubits(int numQubits);
 /* Tuning knobs.  Any build: "fuse_blocks" (compose gate pairs into 4x4
  * blocks before scheduling), "verify" (debug: re-run every fused flush op by
  * op on a shadow copy of the state and exit with a report if the results
- * differ; env QUEST_VERIFY=1, tolerance QUEST_VERIFY_TOL).  HIP build:
- * "direct_kernels" (LDS-free kernel for a pass holding one gate), "tile_mode"
- * (0 op by op, 1 register phases, 2 dense blocks), "tile_qubits",
- * "tile_wg_per_cu", "direct_layout", "direct_low_to_tile".  Returns 1 if the
- * key is known.  Also settable at start via QUEST_DIRECT_KERNELS /
- * QUEST_TILE_MODE / QUEST_TILE_QUBITS / QUEST_TILE_WG_PER_CU / ... */
+ * differ; env QUEST_VERIFY=1, tolerance QUEST_VERIFY_TOL), "plan_max_ops"
+ * (most ops one fused pass takes, 0 = no limit; env QUEST_PLAN_MAX_OPS),
+ * "wave_relabel".  HIP build: "direct_kernels" (LDS-free kernel for a pass
+ * holding one gate), "tile_mode" (0 op by op, 1 register phases, 2 dense
+ * blocks, 3 wave tiles), "tile_qubits", "tile_wg_per_cu", "wave_wg_per_cu",
+ * "direct_layout" (0 grid-stride, 1 looping runs, 2 one run per workgroup),
+ * "direct_low_to_tile" (1: gates on bits inside a 128-byte line go to the tile
+ * pass).  Returns 1 if the key is known.  Also settable at start via
+ * QUEST_DIRECT_KERNELS / QUEST_TILE_MODE / QUEST_TILE_QUBITS /
+ * QUEST_TILE_WG_PER_CU / ...
+ *
+ * Start-up only (HIP build): QUEST_IM_GAP (bytes between a register's re and
+ * im arrays when they are 1 GiB or larger, default 8 GiB, taken only when a
+ * tenth of the device stays free), QUEST_ALLOC_MODE (0 two allocations, 1
+ * joint with QUEST_IM_OFFSET, 2 physically contiguous, 3 mapped address range
+ * with QUEST_IM_DIST; experiments).  Any build: QUEST_DEPHASE_DIAG=0 keeps
+ * dephasing channels in channel form instead of diagonal ops. */
 int setQuESTTuning(const char* key, int value);
 /* Current value of a tuning knob (into *value); returns 1 if the key is known. */
 int getQuESTTuning(const char* key, int* value);
