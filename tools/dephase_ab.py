@@ -28,7 +28,8 @@ def main():
     out = {}
     for name, fn, cnt in (("damping", lambda: [d.damping(q, 0.1) for q in range(n)], n),
                           ("dephase", lambda: [d.dephase(q, 0.1) for q in range(n)], n),
-                          ("dephase2", lambda: [d.dephase2(q, q + 1, 0.1) for q in range(0, n - 1, 2)], n // 2)):
+                          ("dephase2", lambda: [d.dephase2(q, q + 1, 0.1) for q in range(0, n - 1, 2)], n // 2),
+                          ("depolarise2", lambda: [d.depolarise2(q, q + 1, 0.1) for q in range(0, n - 1, 2)], n // 2)):
         best = 1e9
         for _ in range(2):
             capi.resetQuESTStats()
@@ -39,7 +40,8 @@ def main():
             best = min(best, (time.perf_counter() - t0) / cnt)
         out[name] = (best, capi.getQuESTStats()["passes"])
     mode = os.environ.get("QUEST_DEPHASE_DIAG", "1")
-    print(f"density n={n} QUEST_DEPHASE_DIAG={mode}: " +
+    tq = os.environ.get("QUEST_TILE_QUBITS", "default")
+    print(f"density n={n} QUEST_DEPHASE_DIAG={mode} QUEST_TILE_QUBITS={tq}: " +
           ", ".join(f"{k} {1e3 * v[0]:.2f} ms/channel ({v[1]} passes)" for k, v in out.items()) +
           f", trace {d.total_prob():.12f}", flush=True)
     d.close()
