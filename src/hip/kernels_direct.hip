@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
                 for (int e = 0; e < VN; e++) {
                     if (e & (1 << TT)) continue;
                     if ((((unsigned)at[k] + e) & ib.predMask) != ib.predMask) continue;
-                            mat2apply(m, pr[e], pi[e], pr[e | (1 << TT)], pi[e | (1 << TT)]);
+                    mat2apply(m, pr[e], pi[e], pr[e | (1 << TT)], pi[e | (1 << TT)]);
                 }
             };
             if (VN == 2 || t == 0)
