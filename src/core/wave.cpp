@@ -328,7 +328,9 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // of 64 lanes then spans the fewest DRAM pages and translations
     // (QUEST_WAVE_LANE_ORDER=0: in need order instead)
     // (QUEST_WAVE_LANE_ORDER=2: the wave bits -- LDS transpositions -- take the
-    // latest-needed of the rest first, lanes 3-5 the others by position)
+    // latest-needed of the rest first, lanes 3-5 the others by position.
+    // EXPERIMENTAL, wrong results: a 24-qubit layered circuit came out with
+    // norm 1.0022 under it (tests/test_gpu.py checkpoint test); not a default)
     static const int laneOrder = getenv("QUEST_WAVE_LANE_ORDER") ? atoi(getenv("QUEST_WAVE_LANE_ORDER")) : 1;
     if (laneOrder == 2) {
         std::vector<int> byNeed(rest);  // need order already; latest last
