@@ -33,9 +33,12 @@ void setFusionMaxQubits(int numQubits);
  * op on a shadow copy of the state and exit with a report if the results
  * differ; env QUEST_VERIFY=1, tolerance QUEST_VERIFY_TOL), "plan_max_ops"
  * (most ops one fused pass takes, 0 = no limit; env QUEST_PLAN_MAX_OPS),
- * "wave_relabel".  HIP build: "direct_kernels" (LDS-free kernel for a pass
+ * "wave_relabel", "wave_lane_order" (0 need order, 1 lanes by position, 2
+ * wave bits latest-needed), "wave_shadow" (debug: check every wave pass
+ * against the host emulation; env QUEST_WAVE_SHADOW=1).  HIP build: "direct_kernels" (LDS-free kernel for a pass
  * holding one gate), "tile_mode" (0 op by op, 1 register phases, 2 dense
  * blocks, 3 wave tiles), "tile_qubits", "tile_wg_per_cu", "wave_wg_per_cu",
+ * "wave_tile_map" (XCD-aware tile order of the wave kernel),
  * "direct_layout" (0 grid-stride, 1 looping runs, 2 one run per workgroup),
  * "direct_low_to_tile" (1: gates on bits inside a 128-byte line go to the tile
  * pass).  Returns 1 if the key is known.  Also settable at start via
@@ -115,6 +118,8 @@ typedef struct QuESTStats {
     long long globalDiags;    /* diagonal one-qubit gates on rank qubits applied as per-rank scalings */
     long long flushes;        /* backend queue flushes (each planned into fused passes) */
     long long marginalPasses; /* one-pass computations of every qubit's marginal (calcProbOfOutcome cache) */
+    long long waveShadowChecks;     /* wave passes compared with the host emulation (tuning "wave_shadow") */
+    long long waveShadowMismatches; /* ... that differed from it */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

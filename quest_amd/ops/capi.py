@@ -81,7 +81,8 @@ class _Binding:
             _fields_ = [(n, C.c_longlong) for n in
                         ("opsQueued", "passes", "fusedOps", "swaps", "bytesExchanged", "reductions",
                          "verifiedFlushes", "wavePasses", "waveOps", "waveTransposes", "relabels",
-                         "globalDiags", "flushes", "marginalPasses")]
+                         "globalDiags", "flushes", "marginalPasses", "waveShadowChecks",
+                         "waveShadowMismatches")]
 
         self.Complex, self.ComplexMatrix2, self.Vector = Complex, ComplexMatrix2, Vector
         self.ComplexArray, self.QASMLogger, self.Qureg = ComplexArray, QASMLogger, Qureg

@@ -190,6 +190,7 @@ void readEnvConfig() {
     if (const char* f = getenv("QUEST_FUSION")) rt().fusion = atoi(f) != 0;
     if (const char* k = getenv("QUEST_FUSE_QUBITS")) rt().fuseMaxQubits = atoi(k);
     if (const char* v = getenv("QUEST_VERIFY")) rt().verify = atoi(v) != 0;
+    if (const char* v = getenv("QUEST_WAVE_SHADOW")) rt().waveShadow = atoi(v) != 0;
     if (const char* t = getenv("QUEST_VERIFY_TOL")) rt().verifyTol = atof(t);
     if (const char* s = getenv("QUEST_EXCHANGE_SLICE_MB")) {
         long long mb = atoll(s);
@@ -981,6 +982,14 @@ int setQuESTTuning(const char* key, int value) {
         waveRelabel() = value != 0;
         return 1;
     }
+    if (key && !strcmp(key, "wave_lane_order")) {
+        waveLaneOrder() = value;
+        return 1;
+    }
+    if (key && !strcmp(key, "wave_shadow")) {
+        rt().waveShadow = value != 0;
+        return 1;
+    }
     if (key && !strcmp(key, "verify_inject")) {  // fault injection for the verify test
         rt().verifyInject = value != 0;
         return 1;
@@ -999,6 +1008,10 @@ int getQuESTTuning(const char* key, int* value) {
         v = planMaxOps();
     else if (key && !strcmp(key, "wave_relabel"))
         v = waveRelabel() ? 1 : 0;
+    else if (key && !strcmp(key, "wave_lane_order"))
+        v = waveLaneOrder();
+    else if (key && !strcmp(key, "wave_shadow"))
+        v = rt().waveShadow ? 1 : 0;
     else
         known = be::getTuning(key, &v);
     if (known && value) *value = v;
@@ -1010,6 +1023,10 @@ void syncQureg(Qureg qureg) { router::sync(Q(qureg)); }
 
 void copyStateToGPU(Qureg qureg) {
     QuregImpl& q = Q(qureg);
+    // the reference idiom "write qureg.stateVec, then copyStateToGPU": on the
+    // host build stateVec IS the state, so only the cached norm / marginals
+    // (router.cpp) must learn that it changed
+    router::touch(q);
     if (be::stateOnHost() || !q.hostRe) return;
     router::writeChunk(q, q.hostRe, q.hostIm);
 }
@@ -1081,6 +1098,8 @@ void getQuESTStats(QuESTStats* s) {
     s->globalDiags = stats().globalDiags;
     s->flushes = stats().flushes;
     s->marginalPasses = stats().marginalPasses;
+    s->waveShadowChecks = stats().waveShadowChecks;
+    s->waveShadowMismatches = stats().waveShadowMismatches;
 }
 
 void resetQuESTStats(void) { stats() = Stats(); }

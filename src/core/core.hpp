@@ -116,6 +116,12 @@ struct Runtime {
     bool verify = false;
     double verifyTol = 0;  // QUEST_VERIFY_TOL; 0 = 1e-10 (fp64) / 1e-4 (fp32)
     bool verifyInject = false;  // test hook: corrupt the next verified flush once
+    // QUEST_WAVE_SHADOW=1 / tuning "wave_shadow" (HIP build, debug): every
+    // wave pass is also run by the host emulation (src/core/wave_emu.cpp) on a
+    // host copy of the state and the two compared; a mismatch is reported with
+    // the pass's ops and layout, counted (QuESTStats.waveShadowMismatches) and
+    // the emulated state written back, so later passes are checked on their own
+    bool waveShadow = false;
 };
 Runtime& rt();
 

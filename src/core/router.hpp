@@ -88,6 +88,7 @@ struct Stats {
     long long globalDiags = 0;    // diagonal gates on rank qubits done as per-rank scalings
     long long flushes = 0;        // backend queue flushes (each planned into passes)
     long long marginalPasses = 0; // one-pass all-qubit marginals (probZero cache fills)
+    long long waveShadowChecks = 0, waveShadowMismatches = 0;  // rt().waveShadow
 };
 Stats& stats();
 

@@ -191,6 +191,18 @@ bool& waveRelabel() {
     return on;
 }
 
+bool waveStoresInPlace(const WavePass& wp) {
+    if (wp.stFlipLane >> kWaveLanes) return false;   // wave w stores where wave w ^ f loaded
+    for (int l = kWaveLanes; l < kWaveLaneBits; l++)
+        if (wp.pos[wp.ldLane[l]] != wp.stPos[wp.stLane[l]]) return false;
+    return true;
+}
+
+int& waveLaneOrder() {
+    static int order = getenv("QUEST_WAVE_LANE_ORDER") ? atoi(getenv("QUEST_WAVE_LANE_ORDER")) : 1;
+    return order;
+}
+
 bool relabelsLower(const TileProgram& prog) {
     const Stats keep = stats();
     bool ok = true;
@@ -326,12 +338,10 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     std::vector<int> lanes, waves;
     // lanes 3-5 take the lowest positions of the rest: a 16-byte load / store
     // of 64 lanes then spans the fewest DRAM pages and translations
-    // (QUEST_WAVE_LANE_ORDER=0: in need order instead)
-    // (QUEST_WAVE_LANE_ORDER=2: the wave bits -- LDS transpositions -- take the
-    // latest-needed of the rest first, lanes 3-5 the others by position.
-    // EXPERIMENTAL, wrong results: a 24-qubit layered circuit came out with
-    // norm 1.0022 under it (tests/test_gpu.py checkpoint test); not a default)
-    static const int laneOrder = getenv("QUEST_WAVE_LANE_ORDER") ? atoi(getenv("QUEST_WAVE_LANE_ORDER")) : 1;
+    // (lane order 0: in need order instead; 2: the wave bits -- LDS
+    // transpositions -- take the latest-needed of the rest first, lanes 3-5
+    // the others by position)
+    const int laneOrder = waveLaneOrder();
     if (laneOrder == 2) {
         std::vector<int> byNeed(rest);  // need order already; latest last
         std::vector<int> wv;
@@ -837,6 +847,12 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     for (int s = 0; s < kWaveSlots; s++) wp.stSlot[s] = lay.slotBit[s];
     for (int l = 0; l < kWaveLaneBits; l++) wp.stLane[l] = lay.laneBit[l];
     wp.opEnd = (int)out.ops.size();
+    for (int o = wp.opBegin; o < wp.opEnd; o++)
+        wp.waveExchange = wp.waveExchange || (out.ops[(size_t)o].kind == (int)WKind::TR && out.ops[(size_t)o].b >= kWaveLanes);
+    // QUEST_WAVE_NO_STORE_BARRIER=1 (test hook): plan as before round 3, to
+    // show that the emulation's wave-by-wave schedule catches the race
+    static const bool noBarrier = getenv("QUEST_WAVE_NO_STORE_BARRIER") && atoi(getenv("QUEST_WAVE_NO_STORE_BARRIER"));
+    wp.storeBarrier = !wp.waveExchange && !waveStoresInPlace(wp) && !noBarrier;
     out.passes.push_back(wp);
     stats().waveOps += wp.opEnd - wp.opBegin;
     for (int o = wp.opBegin; o < wp.opEnd; o++) stats().waveTransposes += out.ops[o].kind == (int)WKind::TR;

@@ -130,7 +130,19 @@ struct WavePass {
     // 0-5 and the wave bits above them)
     unsigned stFlip = 0, stFlipLane = 0;
     int stLane[kWaveLaneBits];
+    // The waves of a workgroup run unsynchronised between their loads and
+    // stores unless a wave-bit transposition (LDS, two barriers) lies between.
+    // A pass whose store moves a tile bit held by a wave bit to another
+    // position (relabelling, or a deferred X on a wave bit) has each wave
+    // store onto addresses other waves load: the kernel then waits at a
+    // barrier before the stores (launch record, tileMap bit 30).
+    bool storeBarrier = false;
+    bool waveExchange = false;  // the pass has a wave-bit transposition (its barriers order loads before stores)
 };
+
+// Whether every wave of a tile stores to exactly the addresses it loaded
+// (false: the pass needs storeBarrier or a wave-bit transposition).
+bool waveStoresInPlace(const WavePass& wp);
 
 struct WaveProgram {
     std::vector<WavePass> passes;
@@ -160,5 +172,17 @@ void applyProgramPerm(QuregImpl& q, const TileProgram& prog);
 // (for the planner's statistics and tests).
 int waveTransposeCost(int laneBit);
 extern long long g_waveStoreTrCost;   // planner study: weighted transpositions for the store layout
+
+// Load layout of the bits beyond the slots (QUEST_WAVE_LANE_ORDER / tuning
+// "wave_lane_order"): 1 (default) lanes 3-5 take the lowest positions, 0 need
+// order, 2 the wave bits take the latest-needed bits.
+int& waveLaneOrder();
+
+// Host emulation of one wave pass on a host copy of the state
+// (src/core/wave_emu.cpp): the CPU backend's wave planner mode and the HIP
+// backend's per-pass shadow oracle.
+void emulateWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps);
+// QUEST_WAVE_DUMP: the pass's op mix (and with =2 its handlers) on stderr
+void dumpWavePass(const WaveProgram& wp, const WavePass& ps);
 
 }  // namespace qa

@@ -310,312 +310,11 @@ void runTilePass(real* re, real* im, int L, const TileProgram& prog, const TileP
     }
 }
 
-// Wave-tile emulation: 64 lanes x waves x 2^kWaveSlots registers per tile, exactly the
-// data movement of the GPU wave kernel (src/hip/kernels_wave.hip), so the
-// planner's transpositions and layouts are validated on CPU.
-constexpr int kWaveRegs = 1 << kWaveSlots;
-constexpr int kVLanes = 1 << kWaveLaneBits;  // 64 lanes x the waves sharing a tile
-
-void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) {
-    const WKind kind = (WKind)w.kind;
-    if (kind == WKind::TR) {
-        const int s = w.a, l = w.b;
-        for (int j = 0; j < kWaveRegs; j++) {
-            if ((j >> s) & 1) continue;
-            const int f = j | (1 << s);
-            for (int L0 = 0; L0 < kVLanes; L0++) {
-                if ((L0 >> l) & 1) continue;
-                const int L1 = L0 | (1 << l);
-                std::swap(vr[L1][j], vr[L0][f]);
-                std::swap(vi[L1][j], vi[L0][f]);
-            }
-        }
-        return;
-    }
-    const real* m = w.m;
-    // the shear rotation of tools/gen_wave_asm.py rot(): same operation order
-    auto rot = [&](real& x, real& y, bool neg) {
-        const real t = neg ? -m[0] : m[0], sn = neg ? -m[1] : m[1];
-        x = std::fma(-t, y, x);
-        y = std::fma(sn, x, y);
-        x = std::fma(-t, y, x);
-    };
-    if (kind >= WKind::LM2R && kind <= WKind::LSWAP) {
-        // target on lane bit a: lane pairs (L0, L1 = L0 | 2^a), per register
-        const int a = w.a;
-        for (int L0 = 0; L0 < kVLanes; L0++) {
-            if ((L0 >> a) & 1) continue;
-            if ((((unsigned)L0 ^ w.fLane) & w.cLane) != w.cLane || ((unsigned)L0 & w.cLaneZero)) continue;
-            const int L1 = L0 | (1 << a);
-            for (int j = 0; j < kWaveRegs; j++) {
-                if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
-                const real r0 = vr[L0][j], i0 = vi[L0][j], r1 = vr[L1][j], i1 = vi[L1][j];
-                real *R0 = &vr[L0][j], *I0 = &vi[L0][j], *R1 = &vr[L1][j], *I1 = &vi[L1][j];
-                switch (kind) {
-                    case WKind::LM2R:
-                        *R0 = m[0] * r0 + m[1] * r1;
-                        *I0 = m[0] * i0 + m[1] * i1;
-                        *R1 = m[2] * r0 + m[3] * r1;
-                        *I1 = m[2] * i0 + m[3] * i1;
-                        break;
-                    case WKind::LM2RI:
-                        *R0 = m[0] * r0 - m[1] * i1;
-                        *I0 = m[0] * i0 + m[1] * r1;
-                        *R1 = m[3] * r1 - m[2] * i0;
-                        *I1 = m[3] * i1 + m[2] * r0;
-                        break;
-                    case WKind::LANTI:
-                        *R0 = m[0] * r1 - m[1] * i1;
-                        *I0 = m[0] * i1 + m[1] * r1;
-                        *R1 = m[2] * r0 - m[3] * i0;
-                        *I1 = m[2] * i0 + m[3] * r0;
-                        break;
-                    default:  // LSWAP
-                        *R0 = r1;
-                        *I0 = i1;
-                        *R1 = r0;
-                        *I1 = i0;
-                        break;
-                }
-            }
-        }
-        return;
-    }
-    for (int lane = 0; lane < kVLanes; lane++) {
-        if ((((unsigned)lane ^ w.fLane) & w.cLane) != w.cLane) continue;
-        if ((unsigned)lane & w.cLaneZero) continue;
-        real* r = vr[lane];
-        real* i = vi[lane];
-        if (kind == WKind::CH1 || kind == WKind::CHD) {
-            const int a = w.a, b = w.b;
-            for (int j = 0; j < kWaveRegs; j++) {
-                if (((j >> a) & 1) || ((j >> b) & 1)) continue;
-                const int x1 = j | (1 << a), x2 = j | (1 << b), x3 = x1 | (1 << b);
-                for (real* v : {r, i}) {
-                    v[x1] *= m[4];
-                    v[x2] *= m[4];
-                    if (kind == WKind::CH1) {
-                        const real t = m[2] * v[j];
-                        v[j] = std::fma(m[1], v[x3], m[0] * v[j]);
-                        v[x3] = std::fma(m[3], v[x3], t);
-                    }
-                }
-            }
-            continue;
-        }
-        if (kind >= WKind::DROT && kind <= WKind::DROTN) {
-            for (int j = 0; j < kWaveRegs; j++) {
-                if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
-                real &x = r[j], &y = i[j];
-                if (kind == WKind::DNEG || kind == WKind::DROTN) x = -x, y = -y;
-                if (kind == WKind::DROT || kind == WKind::DROTN) rot(x, y, false);
-                if (kind == WKind::DMULI) {
-                    const real t = x;
-                    x = -y;
-                    y = t;
-                } else if (kind == WKind::DMULNI) {
-                    const real t = x;
-                    x = y;
-                    y = -t;
-                }
-            }
-            continue;
-        }
-        if (kind == WKind::DIAG || kind == WKind::D2S || kind == WKind::D2L) {
-            for (int j = 0; j < kWaveRegs; j++) {
-                if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
-                real tr = m[0], ti = m[1];
-                if (kind == WKind::D2S && ((j >> w.a) & 1)) tr = m[2], ti = m[3];
-                if (kind == WKind::D2L && ((lane >> w.a) & 1)) tr = m[2], ti = m[3];
-                const real x = r[j], y = i[j];
-                r[j] = tr * x - ti * y;
-                i[j] = tr * y + ti * x;
-            }
-            continue;
-        }
-        const int a = w.a;
-        for (int j = 0; j < kWaveRegs; j++) {
-            if ((j >> a) & 1) continue;
-            if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
-            const int f = j | (1 << a);
-            const real r0 = r[j], i0 = i[j], r1 = r[f], i1 = i[f];
-            switch (kind) {
-                case WKind::M2:
-                    r[j] = m[0] * r0 - m[1] * i0 + m[2] * r1 - m[3] * i1;
-                    i[j] = m[0] * i0 + m[1] * r0 + m[2] * i1 + m[3] * r1;
-                    r[f] = m[4] * r0 - m[5] * i0 + m[6] * r1 - m[7] * i1;
-                    i[f] = m[4] * i0 + m[5] * r0 + m[6] * i1 + m[7] * r1;
-                    break;
-                case WKind::M2R:
-                    r[j] = m[0] * r0 + m[1] * r1;
-                    i[j] = m[0] * i0 + m[1] * i1;
-                    r[f] = m[2] * r0 + m[3] * r1;
-                    i[f] = m[2] * i0 + m[3] * i1;
-                    break;
-                case WKind::M2RI:
-                    r[j] = m[0] * r0 - m[1] * i1;
-                    i[j] = m[0] * i0 + m[1] * r1;
-                    r[f] = m[3] * r1 - m[2] * i0;
-                    i[f] = m[3] * i1 + m[2] * r0;
-                    break;
-                case WKind::ANTI:
-                    r[j] = m[0] * r1 - m[1] * i1;
-                    i[j] = m[0] * i1 + m[1] * r1;
-                    r[f] = m[2] * r0 - m[3] * i0;
-                    i[f] = m[2] * i0 + m[3] * r0;
-                    break;
-                case WKind::SWAP:
-                    r[j] = r1;
-                    i[j] = i1;
-                    r[f] = r0;
-                    i[f] = i0;
-                    break;
-                case WKind::ROTY:
-                    rot(r[j], r[f], false);
-                    rot(i[j], i[f], false);
-                    break;
-                case WKind::ROTX:
-                    rot(i[j], r[f], false);
-                    rot(r[j], i[f], true);
-                    break;
-                case WKind::HADD:
-                    r[f] = r0 - r1;
-                    r[j] = std::fma((real)2, r0, -r[f]);
-                    i[f] = i0 - i1;
-                    i[j] = std::fma((real)2, i0, -i[f]);
-                    break;
-                case WKind::YSW:  // a -> -i b, b -> i a
-                    r[j] = i1;
-                    i[j] = -r1;
-                    r[f] = -i0;
-                    i[f] = r0;
-                    break;
-                case WKind::YSWC:
-                    r[j] = -i1;
-                    i[j] = r1;
-                    r[f] = i0;
-                    i[f] = -r0;
-                    break;
-                default: break;
-            }
-        }
-    }
-}
-
-long long g_trCost = 0;  // QUEST_WAVE_DUMP: weighted transposition cost (planner study)
-
-// QUEST_WAVE_DUMP (planner study): the op mix of every wave pass on stderr
-static void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
-    static const bool dump = getenv("QUEST_WAVE_DUMP") != nullptr;
-    if (!dump) return;
-    // QUEST_WAVE_DUMP=2: the GPU handler of every op (names of
-    // tools/gen_wave_asm.py, for tools/wave_cost.py)
-    static const bool perOp = atoi(getenv("QUEST_WAVE_DUMP")) == 2;
-    static const char* kName[] = {"M2", "M2R", "M2RI", "ANTI", "SWAP", "DIAG", "D2S", "D2L", "TR", "LM2R", "LM2RI",
-                                  "LANTI", "LSWAP", "ROTY", "ROTX", "HADD", "YSW", "YSWC", "DROT", "DNEG", "DMULI",
-                                  "DMULNI", "DROTN", "CH1", "CHD"};
-    for (int i = ps.opBegin; i < ps.opEnd && perOp; i++) {
-        const WaveOp& w = wp.ops[(size_t)i];
-        const unsigned lanes = w.cLane & 63u;
-        const int ctrl = (w.cReg | lanes) == 0 ? 0 : (w.cReg == 0 ? 2 : 1);
-        const char* k = kName[w.kind];
-        switch ((WKind)w.kind) {
-            case WKind::TR:
-                if (w.b < kWaveLanes) fprintf(stderr, "H wh_TR_s%d_l%d\n", w.a, w.b);
-                else fprintf(stderr, "H wh_TRW_s%d_b%d\n", w.a, w.b - kWaveLanes);
-                break;
-            case WKind::DIAG: case WKind::DROT: case WKind::DNEG: case WKind::DMULI: case WKind::DMULNI:
-            case WKind::DROTN:
-                fprintf(stderr, "H wh_%s_m%u_l%d\n", k, w.cReg, lanes ? 1 : 0);
-                break;
-            case WKind::D2L: fprintf(stderr, "H wh_D2L_c%d\n", ctrl ? 1 : 0); break;
-            case WKind::LM2R: case WKind::LM2RI: case WKind::LANTI: case WKind::LSWAP:
-                fprintf(stderr, "H wh_%s_l%d_c%d\n", k, w.a, ctrl ? 1 : 0);
-                break;
-            case WKind::CH1: case WKind::CHD: fprintf(stderr, "H wh_%s_a%d_b%d\n", k, w.a, w.b); break;
-            default: fprintf(stderr, "H wh_%s_s%d_c%d\n", k, w.a, ctrl); break;
-        }
-    }
-    int cnt[32] = {0}, trw = 0, ctl = 0;
-    for (int i = ps.opBegin; i < ps.opEnd; i++) {
-        const WaveOp& w = wp.ops[(size_t)i];
-        cnt[w.kind]++;
-        if (w.kind == (int)WKind::TR && w.b >= kWaveLanes) trw++;
-        if (w.kind == (int)WKind::TR) g_trCost += waveTransposeCost(w.b);
-        if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
-    }
-    fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d "
-            "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d chan %d\n",
-            ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
-            cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
-            cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24]);
-    int trb[16] = {0};
-    for (int i = ps.opBegin; i < ps.opEnd; i++)
-        if (wp.ops[(size_t)i].kind == (int)WKind::TR) trb[wp.ops[(size_t)i].b & 15]++;
-    fprintf(stderr, "wave: TR per bit:");
-    for (int b = 0; b < 9; b++) fprintf(stderr, " %d", trb[b]);
-    fprintf(stderr, "\nwave: cumulative weighted transposition cost %lld (store layout %lld)\n", g_trCost,
-            g_waveStoreTrCost);
-}
-
-void runWavePass(real* re, real* im, int L, const WaveProgram& wp, const WavePass& ps) {
-    // shared by the threads of the parallel region below (a thread_local
-    // table here was filled by the calling thread only)
-    std::vector<i64> ldv((size_t)kVLanes * kWaveRegs), stv(ldv.size());
-    auto ld = reinterpret_cast<i64(*)[kWaveRegs]>(ldv.data());
-    auto st = reinterpret_cast<i64(*)[kWaveRegs]>(stv.data());
-    auto offsetOf = [&](const int* pos, const int* slotBit, const int* laneBit, int lane, int j) {
-        i64 off = 0;
-        for (int s = 0; s < kWaveSlots; s++)
-            if ((j >> s) & 1) off |= (i64)1 << pos[slotBit[s]];
-        for (int l = 0; l < kWaveLaneBits; l++)
-            if ((lane >> l) & 1) off |= (i64)1 << pos[laneBit[l]];
-        return off;
-    };
-    for (int lane = 0; lane < kVLanes; lane++)
-        for (int j = 0; j < kWaveRegs; j++) {
-            ld[lane][j] = offsetOf(ps.pos, ps.ldSlot, ps.ldLane, lane, j);
-            // relabelling passes store permuted; pending exchanges (stFlip)
-            // store register j where its partner belongs
-            st[lane][j] = offsetOf(ps.stPos, ps.stSlot, ps.stLane, lane ^ (int)ps.stFlipLane, j ^ (int)ps.stFlip);
-        }
-    dumpWavePass(wp, ps);
-    TilePass tp;
-    tp.k = kWaveBits;
-    for (int b = 0; b < kWaveBits; b++) tp.pos[b] = ps.pos[b];
-    const i64 tiles = (i64)1 << (L - kWaveBits);
-#pragma omp parallel if (((i64)1 << L) >= kOmpMin)
-    {
-        std::vector<real> bufR(kVLanes * kWaveRegs), bufI(kVLanes * kWaveRegs);
-        real(*vr)[kWaveRegs] = reinterpret_cast<real(*)[kWaveRegs]>(bufR.data());
-        real(*vi)[kWaveRegs] = reinterpret_cast<real(*)[kWaveRegs]>(bufI.data());
-#pragma omp for schedule(static)
-        for (i64 T = 0; T < tiles; T++) {
-            const i64 base = tileBase(tp, T, L);
-            for (int lane = 0; lane < kVLanes; lane++)
-                for (int j = 0; j < kWaveRegs; j++) {
-                    vr[lane][j] = re[base + ld[lane][j]];
-                    vi[lane][j] = im[base + ld[lane][j]];
-                }
-            for (int o = ps.opBegin; o < ps.opEnd; o++) {
-                const WaveOp& w = wp.ops[o];
-                if (((u64)base & w.ctrlOut) != w.ctrlOut) continue;
-                applyWaveOp(w, vr, vi);
-            }
-            for (int lane = 0; lane < kVLanes; lane++)
-                for (int j = 0; j < kWaveRegs; j++) {
-                    re[base + st[lane][j]] = vr[lane][j];
-                    im[base + st[lane][j]] = vi[lane][j];
-                }
-        }
-    }
-}
-
 void runProgram(real* re, real* im, int L, const TileProgram& prog, bool wave = false) {
     for (const TilePass& ps : prog.passes) {
         WaveProgram wp;
         if (wave && planWavePass(ps, prog.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, wp)) {
-            runWavePass(re, im, L, wp, wp.passes[0]);
+            emulateWavePass(re, im, L, wp, wp.passes[0]);
             stats().wavePasses++;
         } else {
             runTilePass(re, im, L, prog, ps);

@@ -42,6 +42,7 @@ struct Tuning {
     int directLayout = 2;   // direct kernels: 0 grid-stride units, 1 looping contiguous chunks, 2 one chunk per workgroup
     int directLowToTile = 0;  // 1: ops on bits inside a 128-byte line go to the tile pass (0: in-vector / lane-shuffle kernels)
     int tileQubits = 0;     // tile bits of fused passes (0: kTileQubits; kTileQubits + 1 = 64 KiB tiles)
+    int waveTileMap = 0;    // wave kernel: XCD / CU-aware tile order (QUEST_WAVE_TILE_MAP)
 };
 Tuning& tuning();
 

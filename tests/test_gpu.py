@@ -21,7 +21,7 @@ def genv():
 
 
 _KNOBS = ("tile_mode", "direct_kernels", "tile_qubits", "direct_layout", "direct_low_to_tile", "tile_wg_per_cu",
-          "wave_wg_per_cu", "fuse_blocks", "verify")
+          "wave_wg_per_cu", "fuse_blocks", "verify", "wave_lane_order", "wave_tile_map", "wave_shadow")
 
 
 @pytest.fixture(autouse=True)

@@ -167,3 +167,28 @@ def test_init_pure_and_add_density(env):
     np.testing.assert_allclose(capi.getAmps(d).reshape(8, 8, order="F"), want, atol=1e-12)
     for r in (p, d, d2):
         capi.destroyQureg(r, env.env)
+
+
+def test_host_state_edit_then_copy_to_gpu_refreshes_caches(env):
+    """The reference idiom: write qureg.stateVec directly, then
+    copyStateToGPU.  On the host build stateVec is the live state; the cached
+    norm / marginals must not survive the edit."""
+    q = capi.createQureg(3, env.env)
+    capi.initPlusState(q)
+    assert abs(capi.calcTotalProb(q) - 1) < 1e-12
+    p0 = capi.calcProbOfOutcome(q, 0, 0)
+    assert abs(p0 - 0.5) < 1e-12
+    re = q.stateVec.real
+    for i in range(8):
+        re[i] = 1.0 if i == 0 else 0.0
+        q.stateVec.imag[i] = 0.0
+    capi.copyStateToGPU(q)
+    assert abs(capi.calcTotalProb(q) - 1) < 1e-12
+    assert abs(capi.calcProbOfOutcome(q, 0, 0) - 1) < 1e-12
+    re[0] = 0.0
+    re[1] = 2.0 ** -0.5
+    re[3] = 2.0 ** -0.5
+    capi.copyStateToGPU(q)
+    assert abs(capi.calcProbOfOutcome(q, 0, 1) - 1) < 1e-12
+    assert abs(capi.calcProbOfOutcome(q, 1, 1) - 0.5) < 1e-12
+    capi.destroyQureg(q, env.env)

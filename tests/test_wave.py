@@ -162,3 +162,37 @@ def test_exchange_frame_gpu():
     out = _run(["-c", script, ROOT, "3"], {"QUEST_BACKEND": "hip"}, timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "xframe err" in out.stdout
+
+
+RACE = r'''
+import sys
+import quest_amd as qa
+from quest_amd.models import random_layered
+e = qa.Env()
+r = qa.Register(e, 24)
+r.init_plus()
+random_layered(24, 2, seed=2).apply(r)
+print("norm %.15f" % r.total_prob())
+'''
+
+
+@pytest.mark.parametrize("barrier", [True, False])
+def test_emulation_orders_waves_like_the_kernel(barrier):
+    """Round-2's GPU-only wrong result (lane order 2: <psi|psi> = 1.0022 on
+    the 24-qubit checkpoint circuit) was a race between the waves of a
+    workgroup: a relabelling pass without wave-bit transpositions moved tile
+    bits held by wave bits, so each wave stored onto addresses another wave
+    had not loaded yet.  The emulation now runs such passes wave by wave (the
+    worst legal order) unless the plan carries the store barrier: planned as
+    in round 2 (QUEST_WAVE_NO_STORE_BARRIER=1) it loses unitarity like the
+    kernel did; planned with the barrier it is exact."""
+    env = {"QUEST_BACKEND": "cpu", "QUEST_CPU_PLANNER": "3", "QUEST_WAVE_LANE_ORDER": "2"}
+    if not barrier:
+        env["QUEST_WAVE_NO_STORE_BARRIER"] = "1"
+    out = _run(["-c", RACE], env)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    norm = float(out.stdout.split("norm")[1])
+    if barrier:
+        assert abs(norm - 1) < 1e-11, norm
+    else:
+        assert abs(norm - 1) > 1e-3, norm

@@ -1170,6 +1170,18 @@ class Gen:
         self.label("wh_OPS_DONE")     # the sentinel record's handler
         self.handlers[LAYOUT["done"]] = "wh_OPS_DONE"
         e("s_waitcnt lgkmcnt(0)")      # the prefetch past the last op writes s[36:59]
+        if self.W:
+            # store barrier (launch + 20, bit 30; set by the host for passes
+            # whose store moves wave bits to other positions and that have no
+            # wave-bit transposition): a wave's stores then land on addresses
+            # other waves of the workgroup load, so every wave must have loaded
+            # the tile (its loads completed before its first op) first
+            e("s_load_dword s96, s[8:9], 0x14")
+            e("s_waitcnt lgkmcnt(0)")
+            e("s_bitcmp1_b32 s96, 30")
+            e("s_cbranch_scc0 .Lst_nobar")
+            e("s_barrier")
+            self.label(".Lst_nobar")
         self.wave_bytes(ST_WAVE, 34)
         self.groups("st", 216, vstb, NG, 0, 96)
         e("s_add_u32 s16, s16, s14")
