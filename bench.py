@@ -22,7 +22,14 @@ Besides the headline, a single-GPU run adds (outside the timed region, ~10 s):
     calcProbOfOutcome, 10 getAmp; tutorial_example.c:1-3, 29-534);
   * ``window1_s_per_gate``: the headline circuit flushed after every layer
     (the scheduler sees one layer at a time, as in a program that reads the
-    state between layers).
+    state between layers);
+  * ``q34``: 34 qubits (256 GiB, the largest state one MI355X holds): unfused
+    H on targets 0 / 17 / 33 and a 6-layer random layered circuit;
+  * ``density17``: a 17-qubit density matrix (2^34 amplitudes): damping,
+    dephasing, two-qubit dephasing and depolarising per channel, gates;
+  * ``fp32``: the headline circuit with the QUEST_PREC=1 library (a child
+    process), its s/gate and the ratio to fp64.
+  (--extras q34,fp32 picks some; --no-extras none)
 A multi-GPU run must use RCCL (``--allow-transport`` accepts another one).
 """
 from __future__ import annotations
@@ -48,7 +55,9 @@ def main():
     ap.add_argument("--qubits", type=int, default=30, help="qubits per GPU")
     ap.add_argument("--eager", action="store_true", help="disable gate fusion (one pass per gate)")
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--no-extras", action="store_true", help="skip sweep / fork30 / one-layer window")
+    ap.add_argument("--no-extras", action="store_true", help="skip every extra (single-GPU runs only)")
+    ap.add_argument("--extras", default="window1,fork30,sweep,q34,density17,fp32",
+                    help="comma-separated extras of a single-GPU run")
     ap.add_argument("--allow-transport", action="store_true", help="accept a non-RCCL transport with N > 1")
     args = ap.parse_args()
 
@@ -130,7 +139,11 @@ def main():
     s_per_gate = elapsed / max(gates, 1)
     extras = {}
     if world == 1 and not args.no_extras and qa.capi.getQuESTBackend() == "HIP":
-        extras = run_extras(qa, reg, n, layer_gates, args)
+        extras = run_extras(qa, reg, n, layer_gates, args)   # closes reg
+        if "s_per_gate" in extras.get("fp32", {}):
+            extras["fp32"]["ratio_to_fp64"] = extras["fp32"]["s_per_gate"] / (elapsed / max(gates, 1))
+    else:
+        reg.close()
     result = {
         "metric": "single-qubit-gate time (s) vs #qubits, fp64 state-vector; 1/2/4/8-GPU scaling",
         "value": s_per_gate,
@@ -166,7 +179,6 @@ def main():
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
-    reg.close()
 
 
 def _median_time(fn, reps=5):
@@ -179,60 +191,95 @@ def _median_time(fn, reps=5):
 
 
 def run_extras(qa, reg, n, layer_gates, args):
-    """Sweep, fork30 and one-layer window (single GPU, outside the timed
-    region; see the module docstring)."""
+    """Single-GPU extras, outside the timed region (see the module
+    docstring); closes the bench register before the 256 GiB ones."""
     from quest_amd.models import fork_circuit
     from quest_amd.models.circuits import Circuit
+    from quest_amd.utils.bench_workloads import run_density17, run_q34
 
+    todo = set(args.extras.split(","))
     out = {}
-    # one-layer window: the same layers, flushed one at a time
-    t0 = time.perf_counter()
-    g = 0
-    for s in range(args.steps):
-        Circuit(n, layer_gates[args.warmup + s]).apply(reg)
-        reg.flush()
-        g += len(layer_gates[args.warmup + s])
-    reg.sync()
-    out["window1_s_per_gate"] = (time.perf_counter() - t0) / max(g, 1)
-    # fork program on a fresh register (the bench register stays allocated)
-    fork = fork_circuit()
-    f = qa.Register(reg.envobj, 30)
-    f.init_zero()
-    f.sync()
-    t0 = time.perf_counter()
-    fork.apply(f)
-    f.sync()
-    t1 = time.perf_counter()
-    probs = [f.prob(q, 1) for q in range(30)]
-    t2 = time.perf_counter()
-    amps = [f.amp(i) for i in range(10)]
-    t3 = time.perf_counter()
-    out["fork30"] = {"total_s": t3 - t0, "gates_s": t1 - t0, "probs_s": t2 - t1, "amps_s": t3 - t2,
-                     "gates": len(fork.gates), "p_q0": probs[0], "amp0": [amps[0].real, amps[0].imag]}
-    f.close()
-    # unfused single-qubit gate time vs #qubits
-    qa.capi.setGateFusion(0)
-    sweep = []
-    for m in range(20, 33, 2):
-        r = qa.Register(reg.envobj, m)
-        r.init_plus()
-        r.sync()
-        row = {"n": m}
-        for name, t in (("h0", 0), ("hmid", m // 2), ("htop", m - 1), ("tmid", m // 2)):
-            gate = r.h if name[0] == "h" else r.t
+    if "window1" in todo:
+        # one-layer window: the same layers, flushed one at a time
+        t0 = time.perf_counter()
+        g = 0
+        for s in range(args.steps):
+            Circuit(n, layer_gates[args.warmup + s]).apply(reg)
+            reg.flush()
+            g += len(layer_gates[args.warmup + s])
+        reg.sync()
+        out["window1_s_per_gate"] = (time.perf_counter() - t0) / max(g, 1)
+    if "fork30" in todo:
+        # fork program on a fresh register (the bench register stays allocated)
+        fork = fork_circuit()
+        f = qa.Register(reg.envobj, 30)
+        f.init_zero()
+        f.sync()
+        t0 = time.perf_counter()
+        fork.apply(f)
+        f.sync()
+        t1 = time.perf_counter()
+        probs = [f.prob(q, 1) for q in range(30)]
+        t2 = time.perf_counter()
+        amps = [f.amp(i) for i in range(10)]
+        t3 = time.perf_counter()
+        out["fork30"] = {"total_s": t3 - t0, "gates_s": t1 - t0, "probs_s": t2 - t1, "amps_s": t3 - t2,
+                         "gates": len(fork.gates), "p_q0": probs[0], "amp0": [amps[0].real, amps[0].imag]}
+        f.close()
+    if "sweep" in todo:
+        # unfused single-qubit gate time vs #qubits
+        qa.capi.setGateFusion(0)
+        sweep = []
+        for m in range(20, 33, 2):
+            r = qa.Register(reg.envobj, m)
+            r.init_plus()
+            r.sync()
+            row = {"n": m}
+            for name, t in (("h0", 0), ("hmid", m // 2), ("htop", m - 1), ("tmid", m // 2)):
+                gate = r.h if name[0] == "h" else r.t
 
-            def one():
-                gate(t)
-                r.sync()
+                def one():
+                    gate(t)
+                    r.sync()
 
-            one()  # warm
-            row[name + "_ms"] = 1e3 * _median_time(one)
-        row["hmid_TBps"] = 2 * 16 * (1 << m) / (row["hmid_ms"] * 1e-3) / 1e12
-        sweep.append(row)
-        r.close()
-    qa.capi.setGateFusion(1)
-    out["sweep"] = sweep
+                one()  # warm
+                row[name + "_ms"] = 1e3 * _median_time(one)
+            row["hmid_TBps"] = 2 * 16 * (1 << m) / (row["hmid_ms"] * 1e-3) / 1e12
+            sweep.append(row)
+            r.close()
+        qa.capi.setGateFusion(1)
+        out["sweep"] = sweep
+    env = reg.envobj
+    reg.close()
+    if qa.capi.binding().prec == 2:
+        res = {}
+        if "q34" in todo:
+            run_q34(env, res)
+            out["q34"] = res["q34"]
+        if "density17" in todo:
+            run_density17(env, res)
+            out["density17"] = res["density17"]
+    if "fp32" in todo and qa.capi.binding().prec == 2:
+        out["fp32"] = _run_fp32(args)
     return out
+
+
+def _run_fp32(args):
+    """The headline circuit with the fp32 library, in a child process (a
+    process binds one native library)."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.abspath(__file__), "--no-extras", "--steps", str(args.steps), "--warmup",
+           str(args.warmup), "--qubits", str(args.qubits), "--seed", str(args.seed)]
+    env = dict(os.environ, QUEST_PREC="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    if p.returncode != 0:
+        return {"error": p.stderr[-500:]}
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    return {"s_per_gate": d["value"], "passes": d["config"]["passes"], "norm_error": d["config"]["norm_error"],
+            "unfused_gate_s": d["config"]["unfused_gate_s"], "dtype": d["dtype"]}
 
 
 if __name__ == "__main__":

@@ -24,7 +24,13 @@ VARIANTS = {
     "eager-direct": dict(fusion=0, tile_mode=2, direct_kernels=1),
     "eager-tile": dict(fusion=0, tile_mode=2, direct_kernels=0),
 }
-DEFAULTS = {"tile_mode": 3, "direct_kernels": 1, "tile_wg_per_cu": 2, "fuse_blocks": 1, "tile_qubits": 0}
+# wave planner / kernel knobs (round 3: runtime tuning keys)
+for _lo in (0, 1, 2):
+    for _tm in (0, 1):
+        VARIANTS[f"wave-lo{_lo}-tm{_tm}"] = dict(fusion=1, tile_mode=3, direct_kernels=1, wave_lane_order=_lo,
+                                                 wave_tile_map=_tm)
+DEFAULTS = {"tile_mode": 3, "direct_kernels": 1, "tile_wg_per_cu": 2, "fuse_blocks": 1, "tile_qubits": 0,
+            "wave_lane_order": 1, "wave_tile_map": 0}
 
 
 def main():
