@@ -88,7 +88,12 @@ bool memoryBudget(int nSV, const char* caller) {
         freeB = (size_t)atoll(e) << 20;
         known = true;
     }
-    if (!known || (long long)freeB >= m.total) return true;
+    int fits = !known || (long long)freeB >= m.total;
+    // every rank takes the same decision (ranks sharing one GPU see
+    // different free amounts): one rank returning an empty Qureg while the
+    // others go on into collectives would hang the job
+    if (comm::active()) fits = comm::allreduceAnd(fits);
+    if (fits) return true;
     char detail[256];
     const double G = 1024.0 * 1024 * 1024;
     snprintf(detail, sizeof detail,
@@ -785,9 +790,14 @@ void addDensityMatrix(Qureg combineQureg, qreal otherProb, Qureg otherQureg) {
 // ops (their inverse powers stay well inside the range of qreal); stronger
 // dephasing keeps the channel form.
 // QUEST_DEPHASE_DIAG=0 keeps the channel forms (A/B).
+// fp64 only: the diagonal form multiplies the populations by factors whose
+// product is 1 only up to rounding (two factors for one qubit, fifteen up to
+// g^-4 for two), about 1e-16 relative in fp64 but 1e-7 in fp32, where the
+// channel forms (which never touch the populations) are kept.
 constexpr double kDiagDephaseMin = 1e-3;
 bool dephaseDiag() {
-    static const bool on = !getenv("QUEST_DEPHASE_DIAG") || atoi(getenv("QUEST_DEPHASE_DIAG")) != 0;
+    static const bool on = sizeof(real) == 8 &&
+                           (!getenv("QUEST_DEPHASE_DIAG") || atoi(getenv("QUEST_DEPHASE_DIAG")) != 0);
     return on;
 }
 

@@ -2,7 +2,8 @@
 // reference seeds and draws measurement outcomes from (QuEST/src/mt19937ar.c:
 // init_by_array :80, genrand_real1 :150).  Re-implemented here; the output
 // sequence is bit-identical to the canonical algorithm, which the golden test
-// tests/test_rng.py pins (seedQuEST.test:9-15 in the reference).
+// tests/test_reference_suite.py::test_seed_quest_mt19937_golden pins
+// (seedQuEST.test:9-15 in the reference).
 //
 // One generator per process; every rank seeds it identically, so all ranks
 // draw the same measurement outcome without communicating.

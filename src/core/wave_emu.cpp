@@ -215,7 +215,14 @@ void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
     if (!dump) return;
     // QUEST_WAVE_DUMP=2: the GPU handler of every op (names of
     // tools/gen_wave_asm.py, for tools/wave_cost.py)
-    static const bool perOp = atoi(getenv("QUEST_WAVE_DUMP")) == 2;
+    static const bool perOp = atoi(getenv("QUEST_WAVE_DUMP")) >= 2;
+    // QUEST_WAVE_DUMP=3: also every op's fields (planner studies)
+    static const bool fields = atoi(getenv("QUEST_WAVE_DUMP")) == 3;
+    for (int i = ps.opBegin; i < ps.opEnd && fields; i++) {
+        const WaveOp& w = wp.ops[(size_t)i];
+        fprintf(stderr, "O %d %d %d %x %x %x %llx\n", w.kind, w.a, w.b, w.cReg, w.cLane, w.cLaneZero,
+                (unsigned long long)w.ctrlOut);
+    }
     static const char* kName[] = {"M2", "M2R", "M2RI", "ANTI", "SWAP", "DIAG", "D2S", "D2L", "TR", "LM2R", "LM2RI",
                                   "LANTI", "LSWAP", "ROTY", "ROTX", "HADD", "YSW", "YSWC", "DROT", "DNEG", "DMULI",
                                   "DMULNI", "DROTN", "CH1", "CHD"};

@@ -59,3 +59,40 @@ def test_dephase_fuses_into_one_pass(env):
     reg.sync()
     assert capi.getQuESTStats()["passes"] == 1
     reg.close()
+
+
+FP32_POPS = r'''
+import numpy as np
+import quest_amd as qa
+from quest_amd.ops import capi
+assert capi.getQuEST_PREC() == 1
+e = qa.Env()
+r = qa.Register(e, 5, density=True)
+r.init_plus()
+for q in range(5):
+    r.h(q); r.ry(q, 0.3 * (q + 1))
+r.sync()
+before = r.to_numpy().reshape(32, 32, order="F")
+for q in range(5):
+    r.dephase(q, 0.37)
+for q in range(4):
+    r.dephase2(q, q + 1, 0.61)
+after = r.to_numpy().reshape(32, 32, order="F")
+d0, d1 = np.diag(before), np.diag(after)
+print("pops", np.max(np.abs(d1 - d0)), "trace", abs(np.trace(after) - np.trace(before)))
+assert np.array_equal(d0, d1), np.max(np.abs(d1 - d0))
+'''
+
+
+def test_fp32_dephasing_leaves_populations_untouched():
+    """fp32 keeps the channel forms (ADVICE r2): the populations (diagonal of
+    rho) come out bit for bit unchanged, as in the reference's kernels."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QUEST_PREC="1", QUEST_BACKEND=os.environ.get("QUEST_BACKEND", "cpu"))
+    out = subprocess.run([sys.executable, "-c", FP32_POPS], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
