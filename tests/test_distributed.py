@@ -103,3 +103,32 @@ def test_eight_ranks(env, tmp_path, name):
             assert str(g) == v, k
         else:
             np.testing.assert_allclose(np.asarray(g), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+
+
+def test_bench_under_torchrun_host_build():
+    """bench.py in the driver's launch shape (torch.distributed.run, 4 ranks,
+    127.0.0.1 rendezvous) on the host build: one JSON line from rank 0 with
+    n_gpus 4, the state sharded over 4 ranks and qubit swaps performed."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, QUEST_BACKEND="cpu", OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "QUEST_BOOTSTRAP_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "4", "--qubits", "14", "--steps", "3",
+           "--warmup", "1", "--allow-transport"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["config"]["qubits"] == 16
+    assert d["config"]["swaps"] > 0 and d["config"]["norm_error"] < 1e-10

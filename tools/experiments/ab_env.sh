@@ -1,5 +1,5 @@
 # A/B the headline bench between two environment settings on the same box:
-# bash tools/ab_env.sh "VAR=a" "VAR=b" [rounds]
+# bash tools/experiments/ab_env.sh "VAR=a" "VAR=b" [rounds]
 A=$1; B=$2; N=${3:-2}
 for r in $(seq $N); do
   for v in "$A" "$B"; do

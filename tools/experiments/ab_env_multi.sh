@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B/C... of the headline bench between environment settings on one box:
-# bash tools/ab_env_multi.sh ROUNDS "VAR=a" "VAR=b" "VAR=c" ...
+# bash tools/experiments/ab_env_multi.sh ROUNDS "VAR=a" "VAR=b" "VAR=c" ...
 N=$1; shift
 for r in $(seq $N); do
   for v in "$@"; do

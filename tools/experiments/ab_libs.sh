@@ -1,5 +1,5 @@
 # A/B the headline bench between the in-tree library and another build of it
-# on the same box: bash tools/ab_libs.sh <other.so> [rounds]
+# on the same box: bash tools/experiments/ab_libs.sh <other.so> [rounds]
 OTHER=$1
 N=${2:-2}
 for r in $(seq $N); do

@@ -3,12 +3,12 @@
 (in-vector kernel), 2 (lane-shuffle kernel) and n/2 (pair kernel), and T on
 n/2 (diagonal kernel, half the state), 28 qubits, three of each.
 
-    rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --kernel-trace -- python3 tools/direct_pmc.py
+    rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --kernel-trace -- python3 tools/experiments/direct_pmc.py
 """
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -3,7 +3,7 @@
 H on target 0 and n/2 for several (allocation mode, im offset) placements of
 the re/im arrays and both direct-kernel unit orders.
 
-    python tools/layout_probe.py --qubits 28,29,30,31
+    python tools/experiments/layout_probe.py --qubits 28,29,30,31
 """
 import argparse
 import os
@@ -11,7 +11,7 @@ import statistics
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 PLACEMENTS = [("split", None), ("joint+0", 0), ("joint+4K", 4096), ("joint+1M4K", (1 << 20) + 4096),
               ("joint+2M", 2 << 20), ("joint+64M", 64 << 20)]

@@ -4,14 +4,14 @@ pass with k general one-qubit unitaries (+ CZs that stop them fusing) on
 qubits inside one tile, for growing k.  A flat curve up to some k means the
 ops hide under the stream; a line from k=0 means they add to it.
 
-    python tools/overlap_sweep.py [--qubits 30]
+    python tools/experiments/overlap_sweep.py [--qubits 30]
 """
 import argparse
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -5,7 +5,7 @@ Applies `m` gates on tile qubits 0..10 (so they land in ONE pass) and times
 the pass for each tile mode; also times a torch device copy of the same
 bytes as the streaming floor.
 
-    python tools/pass_cost.py --qubits 30
+    python tools/experiments/pass_cost.py --qubits 30
 """
 import argparse
 import json
@@ -14,7 +14,7 @@ import statistics
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

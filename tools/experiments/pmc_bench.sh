@@ -1,6 +1,6 @@
 # PMC counters of the wave-tile kernel on the headline bench (30 qubits, 3
 # layers), one rocprofv3 pass per counter group (run on the GPU box:
-# bash tools/pmc_bench.sh); summaries -> gpurun_out/pmcb_*
+# bash tools/experiments/pmc_bench.sh); summaries -> gpurun_out/pmcb_*
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 B="$R/bench.py --steps 3 --warmup 1"

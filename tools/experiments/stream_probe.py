@@ -3,14 +3,14 @@
 over the state by each engine with (almost) no arithmetic, next to a plain
 device-to-device copy of the same bytes, all on the same box in one run.
 
-    python tools/stream_probe.py [--qubits 30] [--reps 5]
+    python tools/experiments/stream_probe.py [--qubits 30] [--reps 5]
 """
 import argparse
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

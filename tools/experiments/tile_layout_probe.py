@@ -5,14 +5,14 @@ tile is exactly those qubits; run with QUEST_WAVE_NOOPS=1 the kernel only
 loads and stores (no arithmetic), so the time is the memory system's
 answer to that access pattern (2 x 16 B x 2^n bytes per pass).
 
-    QUEST_WAVE_NOOPS=1 python tools/tile_layout_probe.py [--qubits 30]
+    QUEST_WAVE_NOOPS=1 python tools/experiments/tile_layout_probe.py [--qubits 30]
 """
 import argparse
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -4,7 +4,7 @@ gates of a single kind on the low 10 qubits (all inside one tile) at
 `qubits` qubits, timed against a pass of two phase gates (load + store +
 dispatch only).  ms/op = (t_kind - t_base) / count.
 
-    python tools/wave_micro.py [--qubits 28] [--count 32]
+    python tools/experiments/wave_micro.py [--qubits 28] [--count 32]
 """
 import argparse
 import math
@@ -12,7 +12,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Table of rocprofv3 PMC counters per dispatch of one kernel, merged over
-the passes of a directory tree (tools/pmc_micro.sh):
+the passes of a directory tree (tools/experiments/pmc_micro.sh):
 
     python3 tools/pmc_summary.py gpurun_out/pmcm [--kernel qa_wave_tile]
 
