@@ -801,6 +801,50 @@ bool dephaseDiag() {
     return on;
 }
 
+// Two-qubit channels as one-qubit ops (QUEST_CHAN2_GATES=0: the 16-element
+// channel op of the LDS kernel instead).  In the "differs" frame -- c1 ^= r1,
+// c2 ^= r2 by CNOTs, so c1 / c2 tell whether row and column bits differ --
+// the channels become a phase-free diagonal on the coherences and real 2x2
+// mixes of the populations controlled on c1 = c2 = 0; every op is a wave-
+// engine op (CNOTs, Xs that the wave planner defers to its exchange frame,
+// diagonal factors, controlled real 2x2), so the channels fuse with the gates
+// around them in register-resident passes, and the populations are never
+// multiplied by anything but the channel's own coefficients.
+bool twoQubitChannelsAsGates() {
+    static const bool on = !getenv("QUEST_CHAN2_GATES") || atoi(getenv("QUEST_CHAN2_GATES")) != 0;
+    return on;
+}
+
+// Enter (undo = false) or leave the differs frame.  Entering leaves c1 and c2
+// flipped (X), so that c1 = c2 = 1 marks the populations.
+void differsFrame(QuregImpl& q, int r1, int r2, int c1, int c2, bool undo) {
+    if (!undo) {
+        router::mat2(q, c1, &r1, 1, kX);
+        router::mat2(q, c2, &r2, 1, kX);
+        router::mat2(q, c1, nullptr, 0, kX);
+        router::mat2(q, c2, nullptr, 0, kX);
+    } else {
+        router::mat2(q, c1, nullptr, 0, kX);
+        router::mat2(q, c2, nullptr, 0, kX);
+        router::mat2(q, c2, &r2, 1, kX);
+        router::mat2(q, c1, &r1, 1, kX);
+    }
+}
+
+// Factor g on the elements with (r1, r2) != (c1, c2): in the differs frame
+// g on c1 = 0 (row and column of qubit 1 differ), then g on c1 = 1, c2 = 0.
+// leave = true returns to the plain frame; false stays in it (c1, c2 flipped).
+void twoQubitDephaseAsGates(QuregImpl& q, int r1, int r2, int c1, int c2, real g, bool leave) {
+    router::mat2(q, c1, &r1, 1, kX);
+    router::mat2(q, c2, &r2, 1, kX);
+    router::diag(q, &c1, 1, {g, 0});                 // qubit 1 differs
+    router::mat2(q, c1, nullptr, 0, kX);
+    const int both[2] = {c1, c2};
+    router::diag(q, both, 2, {g, 0});                // qubit 1 agrees, qubit 2 differs
+    router::mat2(q, c2, nullptr, 0, kX);            // c1 = c2 = 1: populations
+    if (leave) differsFrame(q, r1, r2, c1, c2, true);
+}
+
 void applyOneQubitDephaseError(Qureg qureg, const int targetQubit, qreal prob) {
     if (!v::densMatr(qureg, __func__) || !v::target(qureg, targetQubit, __func__) ||
         !v::oneQubitDephaseProb(prob, __func__))
@@ -850,6 +894,10 @@ void applyTwoQubitDephaseError(Qureg qureg, int qubit1, int qubit2, qreal prob) 
         for (const Term& t : terms) router::diag(q, t.b, t.n, {(real)std::pow((double)g, t.e), 0});
         return;
     }
+    if (twoQubitChannelsAsGates()) {
+        twoQubitDephaseAsGates(q, qubit1, qubit2, qubit1 + q.nRep, qubit2 + q.nRep, g, true);
+        return;
+    }
     router::densChan2(q, qubit1, qubit2, qubit1 + q.nRep, qubit2 + q.nRep, 1 - d, 1, 0);
 }
 
@@ -882,6 +930,35 @@ void applyTwoQubitDepolariseError(Qureg qureg, int qubit1, int qubit2, qreal pro
     real d = (16 * prob) / 15.0;
     if (d == 0) return;
     QuregImpl& q = Q(qureg);
+    if (twoQubitChannelsAsGates()) {
+        // dephasing of the coherences by 1 - d, then the populations of the
+        // pair depolarised: (1 - d) x + d mean = gamma (I + delta X1)(I +
+        // delta X2)(I + delta X1 X2) x with eta = 2 / d, delta = eta - 1 -
+        // sqrt((eta - 1)^2 - 1) (delta / (1 + delta)^2 = d / 4), gamma =
+        // (1 + delta)^-3 -- the reference's
+        // three-step form (QuEST_cpu_local.c:40-51, QuEST_cpu.c:379-480), here
+        // as one-qubit ops in the "differs" frame (see twoQubitDephaseAsGates)
+        // delta as 1 / (a + sqrt(a^2 - 1)), a = eta - 1 (the two roots multiply
+        // to 1): no cancellation for weak channels, where the reference's
+        // difference form loses digits (its "TODO -- test delta too small")
+        const double a = 2 / (double)d - 1;
+        const double delta = 1 / (a + std::sqrt(std::max(0.0, a * a - 1)));
+        const double gamma = 1 / ((1 + delta) * (1 + delta) * (1 + delta));
+        const int r1 = qubit1, r2 = qubit2, c1 = qubit1 + q.nRep, c2 = qubit2 + q.nRep;
+        twoQubitDephaseAsGates(q, r1, r2, c1, c2, 1 - d, false);
+        // populations: c1 = c2 = 1 after the X on both (r1 == c1, r2 == c2)
+        const int ctl[2] = {c1, c2};
+        const cplx mix[4] = {{1, 0}, {(real)delta, 0}, {(real)delta, 0}, {1, 0}};
+        const cplx mixG[4] = {{(real)gamma, 0}, {(real)(gamma * delta), 0}, {(real)(gamma * delta), 0},
+                              {(real)gamma, 0}};
+        router::mat2(q, r1, ctl, 2, mix);     // I + delta X1
+        router::mat2(q, r2, ctl, 2, mix);     // I + delta X2
+        router::mat2(q, r2, &r1, 1, kX);      // X1 X2 -> X1
+        router::mat2(q, r1, ctl, 2, mixG);    // gamma (I + delta X1 X2)
+        router::mat2(q, r2, &r1, 1, kX);
+        differsFrame(q, r1, r2, c1, c2, true);
+        return;
+    }
     router::densChan2(q, qubit1, qubit2, qubit1 + q.nRep, qubit2 + q.nRep, 1 - d, 1 - d, d);
 }
 

@@ -317,6 +317,15 @@ void runProgram(real* re, real* im, int L, const TileProgram& prog, bool wave = 
             emulateWavePass(re, im, L, wp, wp.passes[0]);
             stats().wavePasses++;
         } else {
+            if (wave && getenv("QUEST_WAVE_DUMP")) {
+                fprintf(stderr, "not a wave pass: k %d, %d ops, pos", ps.k, ps.opEnd - ps.opBegin);
+                for (int i = 0; i < ps.k; i++) fprintf(stderr, " %d->%d", ps.pos[i], ps.stPos[i]);
+                fprintf(stderr, ", kinds");
+                for (int o = ps.opBegin; o < ps.opEnd; o++)
+                    fprintf(stderr, " %d(t%d,%d c%llx)", prog.ops[(size_t)o].kind, prog.ops[(size_t)o].t[0],
+                            prog.ops[(size_t)o].t[1], (unsigned long long)prog.ops[(size_t)o].ctrlIn);
+                fprintf(stderr, "\n");
+            }
             runTilePass(re, im, L, prog, ps);
         }
         stats().passes++;

@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--kernel", default="qa_wave_tile")
+    ap.add_argument("--sum", action="store_true", help="one row: every counter summed over the dispatches")
     args = ap.parse_args()
     table = defaultdict(dict)   # dispatch rank -> counter -> value
     names = []
@@ -29,6 +30,16 @@ def main():
             if c not in names:
                 names.append(c)
             table[rank[int(r["Dispatch_Id"])]][c] = table[rank[int(r["Dispatch_Id"])]].get(c, 0.0) + float(r["Counter_Value"])
+    if args.sum:
+        tot = {n: sum(table[k].get(n, 0.0) for k in table) for n in names}
+        for n in names:
+            print(f"{n:28s} {tot[n]:14.4e}")
+        wc = tot.get("SQ_WAVE_CYCLES")
+        if wc:
+            for n in names:
+                if n != "SQ_WAVE_CYCLES" and n != "SQ_BUSY_CYCLES":
+                    print(f"{n + ' / wave cycles':42s} {tot[n] / wc:8.3f}")
+        return
     print("dispatch " + " ".join(f"{n:>22s}" for n in names))
     for k in sorted(table):
         print(f"{k:8d} " + " ".join(f"{table[k].get(n, float('nan')):22.4e}" for n in names))
