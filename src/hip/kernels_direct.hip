@@ -290,7 +290,7 @@ int directGrid(long long units, int unr) {
         QA_HIP_CHECK(hipGetLastError());                                                                       \
     } while (0)
 
-bool launchDirectOp(real* re, real* im, int L, const Op& op) {
+bool launchDirectOp(real* re, real* im, int L, const Op& op, bool launch) {
     constexpr int VN = Vec16<real>::n;
     constexpr int vbits = VN == 2 ? 1 : 2;
     constexpr int LINE = sizeof(real) == 8 ? 4 : 5;  // log2(amps per 128-byte line)
@@ -324,6 +324,7 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
         if (ni > 8) return false;
         for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
         const long long units = (N >> ni) / VN;
+        if (!launch) return true;
         QA_DIRECT_LAUNCH(diagDirectKernel, 4, re, im, units, ib, op.m[0].re, op.m[0].im);
         return true;
     }
@@ -349,16 +350,19 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op) {
         if (!placed) all[na++] = t;
         for (int i = 0; i < na; i++) ib.pos[ib.n++] = all[i];
         const long long units = (N >> na) / VN;
+        if (!launch) return true;
         QA_DIRECT_LAUNCH(mat2DirectKernel, 4, re, im, units, ib, 1ll << t, m);
     } else if (t >= vbits) {
         if (ni > 8) return false;
         for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
         const long long units = (N >> ni) / VN;
+        if (!launch) return true;
         QA_DIRECT_LAUNCH(mat2ShflKernel, 4, re, im, units, ib, t, 1 << (t - vbits), m);
     } else {
         if (ni > 8) return false;
         for (int i = 0; i < ni; i++) ib.pos[ib.n++] = ins[i];
         const long long units = (N >> ni) / VN;
+        if (!launch) return true;
         QA_DIRECT_LAUNCH(mat2LowKernel, 4, re, im, units, ib, t, m);
     }
     return true;

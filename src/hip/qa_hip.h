@@ -127,7 +127,9 @@ struct TileArgs {
 void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps, const TilePhase* dPhases,
                     const real* dMats, int mode);
 // one-op pass as a streaming kernel without LDS; false if not applicable
-bool launchDirectOp(real* re, real* im, int L, const Op& op);
+// Run a single-op pass with an LDS-free streaming kernel if one applies
+// (launch = false: only report whether one does).
+bool launchDirectOp(real* re, real* im, int L, const Op& op, bool launch = true);
 void launchFill(real* re, real* im, i64 n, real vr, real vi);
 void launchInitDebug(real* re, real* im, i64 n, i64 offset);
 void launchFillWhereBit(real* re, real* im, i64 n, int bit, int outcome, real val);

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--layers", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--window1", action="store_true", help="flush after every layer (bench.py window1_s_per_gate)")
     args = ap.parse_args()
     import quest_amd as qa
     from quest_amd.models import random_layered
@@ -42,6 +43,8 @@ def main():
     qa.capi.resetQuESTStats()
     for s in range(args.layers):
         Circuit(n, per[args.warmup + s]).apply(reg)
+        if args.window1:
+            reg.flush()
     reg.flush()
     st = qa.capi.getQuESTStats()
     print(f"qubits {n} layers {args.layers}: passes {st['passes']} wave {st['wavePasses']} "
