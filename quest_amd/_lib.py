@@ -38,13 +38,15 @@ def gpu_visible() -> bool:
 def resolve(backend: str | None = None, prec: int | None = None) -> tuple[str, int, str]:
     backend = (backend or os.environ.get("QUEST_BACKEND", "auto")).lower()
     prec = int(prec or os.environ.get("QUEST_PREC", "2"))
-    if prec not in (1, 2):
-        raise ValueError("QUEST_PREC must be 1 (fp32) or 2 (fp64)")
+    if prec not in (1, 2, 4):
+        raise ValueError("QUEST_PREC must be 1 (fp32), 2 (fp64) or 4 (long double, host build only)")
     if backend == "auto":
-        backend = "hip" if gpu_visible() else "cpu"
+        backend = "cpu" if prec == 4 else ("hip" if gpu_visible() else "cpu")
     if backend not in ("hip", "cpu"):
         raise ValueError(f"unknown QUEST_BACKEND {backend!r}")
-    name = f"libQuEST_{backend}_f{64 if prec == 2 else 32}.so"
+    if prec == 4 and backend != "cpu":
+        raise ValueError("QUEST_PREC=4 (long double) exists for the host build only, as in the reference")
+    name = f"libQuEST_{backend}_f{ {1: 32, 2: 64, 4: 128}[prec] }.so"
     override = os.environ.get("QUEST_LIB")  # e.g. a CMake build's library
     if override:
         return backend, prec, override

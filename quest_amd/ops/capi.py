@@ -37,9 +37,9 @@ class _Binding:
         self.lib = lib
         self.backend = lib._quest_backend
         self.prec = lib._quest_prec
-        qreal = C.c_double if self.prec == 2 else C.c_float
+        qreal = {1: C.c_float, 2: C.c_double, 4: C.c_longdouble}[self.prec]
         self.qreal = qreal
-        self.np_real = np.float64 if self.prec == 2 else np.float32
+        self.np_real = {1: np.float32, 2: np.float64, 4: np.longdouble}[self.prec]
 
         class Complex(C.Structure):
             _fields_ = [("real", qreal), ("imag", qreal)]

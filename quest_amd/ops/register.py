@@ -279,8 +279,14 @@ class Register:
         import torch
 
         b = capi.binding()
-        dt = torch.float64 if b.prec == 2 else torch.float32
         n = self.q.numAmpsPerChunk
+        if b.prec == 4:
+            # long double has no torch dtype: through host buffers, as complex128
+            re = np.empty(n, dtype=b.np_real)
+            im = np.empty(n, dtype=b.np_real)
+            capi._call("copyChunkToBuffers", self.q, re.ctypes.data_as(C.c_void_p), im.ctypes.data_as(C.c_void_p))
+            return torch.complex(torch.from_numpy(re.astype(np.float64)), torch.from_numpy(im.astype(np.float64)))
+        dt = torch.float64 if b.prec == 2 else torch.float32
         if b.backend == "hip":
             re = torch.empty(n, dtype=dt, device="cuda")
             im = torch.empty(n, dtype=dt, device="cuda")
@@ -296,6 +302,11 @@ class Register:
         import torch
 
         b = capi.binding()
+        if b.prec == 4:
+            re = np.ascontiguousarray(t.real.cpu().numpy(), dtype=b.np_real)
+            im = np.ascontiguousarray(t.imag.cpu().numpy(), dtype=b.np_real)
+            capi._call("copyChunkFromBuffers", self.q, re.ctypes.data_as(C.c_void_p), im.ctypes.data_as(C.c_void_p))
+            return
         dt = torch.float64 if b.prec == 2 else torch.float32
         re = t.real.to(dt).contiguous()
         im = t.imag.to(dt).contiguous()

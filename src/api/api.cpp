@@ -790,13 +790,13 @@ void addDensityMatrix(Qureg combineQureg, qreal otherProb, Qureg otherQureg) {
 // ops (their inverse powers stay well inside the range of qreal); stronger
 // dephasing keeps the channel form.
 // QUEST_DEPHASE_DIAG=0 keeps the channel forms (A/B).
-// fp64 only: the diagonal form multiplies the populations by factors whose
+// fp64 / long double only: the diagonal form multiplies the populations by factors whose
 // product is 1 only up to rounding (two factors for one qubit, fifteen up to
 // g^-4 for two), about 1e-16 relative in fp64 but 1e-7 in fp32, where the
 // channel forms (which never touch the populations) are kept.
 constexpr double kDiagDephaseMin = 1e-3;
 bool dephaseDiag() {
-    static const bool on = sizeof(real) == 8 &&
+    static const bool on = sizeof(real) >= 8 &&
                            (!getenv("QUEST_DEPHASE_DIAG") || atoi(getenv("QUEST_DEPHASE_DIAG")) != 0);
     return on;
 }

@@ -18,7 +18,7 @@ Stats& stats() {
 }
 
 void verifyFlush(int qubits, size_t ops, size_t passes, double maxDiff) {
-    const double tol = rt().verifyTol > 0 ? rt().verifyTol : (sizeof(real) == 8 ? 1e-10 : 1e-4);
+    const double tol = rt().verifyTol > 0 ? rt().verifyTol : (sizeof(real) >= 8 ? 1e-10 : 1e-4);
     stats().verifiedFlushes++;
     if (trace::on())
         trace::event("verify", "\"qubits\": %d, \"ops\": %zu, \"passes\": %zu, \"max_diff\": %.3e", qubits, ops,

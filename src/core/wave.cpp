@@ -74,8 +74,8 @@ WaveOp blank(int kind) {
 // the shears of phi - pi and a factor -1 for the pass (`neg`).
 // tolerances for recognising unit-modulus / structured matrices: a few ulps
 // of the build's precision (the matrices arrive in qreal)
-constexpr double kUnitTol = sizeof(real) == 8 ? 1e-14 : 1e-6;
-constexpr double kNearTol = sizeof(real) == 8 ? 1e-15 : 1e-7;
+constexpr double kUnitTol = sizeof(real) >= 8 ? 1e-14 : 1e-6;
+constexpr double kNearTol = sizeof(real) >= 8 ? 1e-15 : 1e-7;
 inline bool unitCircle(double c, double s) { return std::fabs(c * c + s * s - 1) <= kUnitTol; }
 
 void rotParams(double c, double s, real* m, bool* neg) {
