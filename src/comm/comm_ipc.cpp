@@ -202,12 +202,19 @@ void transfer(const comm::Xfer* x, int n, int slot, hipStream_t producer, hipStr
             exit(EXIT_FAILURE);
         }
         const char* src = importBuffer(x[i].peer, t) + t.offset;
-        const hipError_t e = hipMemcpyAsync(x[i].recv, src, x[i].bytes, hipMemcpyDeviceToDevice, stream);
-        if (e != hipSuccess) {
-            fprintf(stderr, "QuEST ipc: rank %d exchange %llu: copy of %zu B from rank %d (buffer id %llu + %llu) "
-                            "failed: %s\n",
-                    g_rank, g_exchanges, x[i].bytes, x[i].peer, t.id, t.offset, hipGetErrorString(e));
-            exit(EXIT_FAILURE);
+        // a streaming kernel pulls through the IPC mapping (the runtime's
+        // blit copies ran at about 1 TB/s next to the packs)
+        static const bool kernelCopy = !getenv("QUEST_IPC_BLIT") || atoi(getenv("QUEST_IPC_BLIT")) == 0;
+        if (kernelCopy) {
+            hipk::launchCopyVec(x[i].recv, src, x[i].bytes, stream);
+        } else {
+            const hipError_t e = hipMemcpyAsync(x[i].recv, src, x[i].bytes, hipMemcpyDeviceToDevice, stream);
+            if (e != hipSuccess) {
+                fprintf(stderr, "QuEST ipc: rank %d exchange %llu: copy of %zu B from rank %d (buffer id %llu + %llu) "
+                                "failed: %s\n",
+                        g_rank, g_exchanges, x[i].bytes, x[i].peer, t.id, t.offset, hipGetErrorString(e));
+                exit(EXIT_FAILURE);
+            }
         }
         g_pending[slot].push_back(x[i].peer);
     }

@@ -100,6 +100,68 @@ __global__ __launch_bounds__(kThreads) void packKernel(T* __restrict__ re, T* __
     }
 }
 
+// The same gather / scatter for the 16-byte-vector case, streamed the way
+// the direct gate kernels stream: each workgroup owns one run of 256 x 4
+// vector units, every thread issues its four re and four im loads before the
+// first store (0.5-1 TB/s with one vector per thread
+// and a grid-stride loop; tools/swap_trace.sh).  `units` is a multiple of
+// 256 x 4 (the launcher falls back to packKernel otherwise).
+template <typename T, bool UNPACK>
+__global__ __launch_bounds__(kThreads) void packRunKernel(T* __restrict__ re, T* __restrict__ im, PackBits pb,
+                                                          long long start, T* __restrict__ br,
+                                                          T* __restrict__ bi) {
+    using V = typename Vec16<T>::type;
+    constexpr int VN = Vec16<T>::n, UNR = 4;
+    const long long u0 = (long long)blockIdx.x * (kThreads * UNR) + threadIdx.x;
+    long long si[UNR], bj[UNR];
+    for (int k = 0; k < UNR; k++) {
+        const long long j = (u0 + k * kThreads) * VN;
+        long long i = start + j;
+        for (int m = 0; m < pb.k; m++) i = ins0(i, pb.pos[m]);
+        si[k] = i | pb.setMask;
+        bj[k] = j;
+    }
+    V vr[UNR], vi[UNR];
+    if constexpr (UNPACK) {
+        for (int k = 0; k < UNR; k++) {
+            vr[k] = *(reinterpret_cast<const V*>(br + bj[k]));
+            vi[k] = *(reinterpret_cast<const V*>(bi + bj[k]));
+        }
+        for (int k = 0; k < UNR; k++) {
+            *(reinterpret_cast<V*>(re + si[k])) = vr[k];
+            *(reinterpret_cast<V*>(im + si[k])) = vi[k];
+        }
+    } else {
+        for (int k = 0; k < UNR; k++) {
+            vr[k] = *(reinterpret_cast<const V*>(re + si[k]));
+            vi[k] = *(reinterpret_cast<const V*>(im + si[k]));
+        }
+        for (int k = 0; k < UNR; k++) {
+            *(reinterpret_cast<V*>(br + bj[k])) = vr[k];
+            *(reinterpret_cast<V*>(bi + bj[k])) = vi[k];
+        }
+    }
+}
+
+// Device-to-device copy of n 16-byte vectors (runs of 256 x 4 per workgroup,
+// plus a tail loop): the IPC transport's pull from a peer's mapped buffer on
+// the same GPU, instead of the runtime's blit (~1 TB/s under contention).
+__global__ __launch_bounds__(kThreads) void copyVecKernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          long long n) {
+    constexpr int UNR = 4;
+    const long long u0 = (long long)blockIdx.x * (kThreads * UNR) + threadIdx.x;
+    if (u0 + (UNR - 1) * kThreads < n) {
+        uint4 v[UNR];
+        for (int k = 0; k < UNR; k++) v[k] = *(src + u0 + k * kThreads);
+        for (int k = 0; k < UNR; k++) *(dst + u0 + k * kThreads) = v[k];
+        return;
+    }
+    for (int k = 0; k < UNR; k++) {
+        const long long u = u0 + k * kThreads;
+        if (u < n) dst[u] = src[u];
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void axpbyKernel(T* __restrict__ ar, T* __restrict__ ai, T alpha,
                                                         const T* __restrict__ br, const T* __restrict__ bi, T beta,
@@ -181,6 +243,16 @@ void launchPackBits(const real* re, const real* im, const int* pos, int k, u64 s
     const bool vec = (k == 0 || (1ll << pb.pos[0]) >= VN) && (start % VN == 0) && (count % VN == 0);
     real* r = const_cast<real*>(re);
     real* m = const_cast<real*>(im);
+    constexpr long long kRun = (long long)kThreads * 4;
+    if (vec && (count / VN) % kRun == 0) {
+        const dim3 grid((unsigned)((count / VN) / kRun));
+        if (unpack)
+            hipLaunchKernelGGL((packRunKernel<real, true>), grid, dim3(kThreads), 0, stream(), r, m, pb, start, br, bi);
+        else
+            hipLaunchKernelGGL((packRunKernel<real, false>), grid, dim3(kThreads), 0, stream(), r, m, pb, start, br, bi);
+        QA_HIP_CHECK(hipGetLastError());
+        return;
+    }
     const int g = gridFor(vec ? count / VN : count);
     if (unpack) {
         if (vec)
@@ -197,6 +269,20 @@ void launchPackBits(const real* re, const real* im, const int* pos, int k, u64 s
             hipLaunchKernelGGL((packKernel<real, false, false>), dim3(g), dim3(kThreads), 0, stream(), r, m, pb,
                                start, count, br, bi);
     }
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+void launchCopyVec(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes % 16 != 0 || ((uintptr_t)dst | (uintptr_t)src) % 16 != 0) {
+        QA_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+        return;
+    }
+    const long long n = (long long)(bytes / 16);
+    const long long per = (long long)kThreads * 4;
+    const long long g = (n + per - 1) / per;
+    if (g <= 0) return;
+    hipLaunchKernelGGL(copyVecKernel, dim3((unsigned)g), dim3(kThreads), 0, st, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), n);
     QA_HIP_CHECK(hipGetLastError());
 }
 

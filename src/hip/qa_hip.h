@@ -133,6 +133,9 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op, bool launch = true)
 void launchFill(real* re, real* im, i64 n, real vr, real vi);
 void launchInitDebug(real* re, real* im, i64 n, i64 offset);
 void launchFillWhereBit(real* re, real* im, i64 n, int bit, int outcome, real val);
+// Device-to-device copy on stream st by a streaming kernel (hipMemcpyAsync
+// for unaligned sizes): the IPC transport's pulls.
+void launchCopyVec(void* dst, const void* src, size_t bytes, hipStream_t st);
 void launchPackBits(const real* re, const real* im, const int* pos, int k, u64 setMask, i64 start, i64 count,
                     real* br, real* bi, bool unpack);
 void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n);
