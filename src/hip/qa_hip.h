@@ -38,7 +38,7 @@ struct Tuning {
     int directKernels = 1;  // LDS-free kernels for single-op passes
     int tileMode = 0;       // fused tiles: 0 op by op, 1 register phases, 2 dense blocks, 3 wave tiles (fp64 default)
     int tileWgPerCU = 2;    // grid of the register-phase tile kernel, per CU
-    int waveWgPerCU = 3;    // grid of the wave-tile kernel: workgroups (2^kWaveWBits waves each) per CU
+    int waveWgPerCU = 0;    // grid of the wave-tile kernel: 0 one workgroup per tile, else workgroups per CU (looping)
     int directLayout = 2;   // direct kernels: 0 grid-stride units, 1 looping contiguous chunks, 2 one chunk per workgroup
     int directLowToTile = 0;  // 1: ops on bits inside a 128-byte line go to the tile pass (0: in-vector / lane-shuffle kernels)
     int tileQubits = 0;     // tile bits of fused passes (0: kTileQubits; kTileQubits + 1 = 64 KiB tiles)
