@@ -16,7 +16,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-_KNOBS = ("tile_mode", "wave_lane_order", "wave_tile_map", "wave_shadow")
+_KNOBS = ("tile_mode", "wave_lane_order", "wave_tile_map", "wave_shadow", "wave_wg_per_cu")
 
 
 @pytest.fixture(scope="module")
@@ -54,22 +54,25 @@ def _run(genv, n, circ, knobs):
 
 
 @pytest.mark.parametrize("depth", [2, 6])
+@pytest.mark.parametrize("grid", [0, 3])
 @pytest.mark.parametrize("tile_map", [0, 1])
 @pytest.mark.parametrize("lane_order", [0, 1, 2])
-def test_lane_order_tile_map_24q(genv, lane_order, tile_map, depth):
+def test_lane_order_tile_map_24q(genv, lane_order, tile_map, grid, depth):
+    """grid 0: one workgroup per tile (default); 3: a persistent grid of three
+    workgroups per CU looping over the tiles (the tile map needs it)."""
     from quest_amd.models import random_layered
 
     n = 24
     circ = random_layered(n, depth, seed=2)
     ref, _ = _run(genv, n, circ, {"tile_mode": 0, "wave_shadow": 0})
     a, st = _run(genv, n, circ, {"tile_mode": 3, "wave_lane_order": lane_order, "wave_tile_map": tile_map,
-                                 "wave_shadow": 1})
+                                 "wave_wg_per_cu": grid, "wave_shadow": 1})
     assert st["wavePasses"] > 0, st
     assert st["waveShadowChecks"] == st["wavePasses"], st
     assert st["waveShadowMismatches"] == 0, st
     # the shadow check repairs a bad pass: compare with the shadow off too
     b, st2 = _run(genv, n, circ, {"tile_mode": 3, "wave_lane_order": lane_order, "wave_tile_map": tile_map,
-                                  "wave_shadow": 0})
+                                  "wave_wg_per_cu": grid, "wave_shadow": 0})
     want = ref.to_numpy()
     for r in (a, b):
         got = r.to_numpy()
