@@ -72,6 +72,10 @@ SWAP64 = _os.environ.get("WAVE_SWAP64", "1") == "1"   # register exchanges as 64
 # per-lane selects: v_cmp_*_e64 into this SGPR pair + v_cndmask_b32_e64 (a
 # v_cndmask_b32_e32 reading vcc issues ~5x slower on gfx950, tools/isa_micro.hip)
 SEL = "s[98:99]"
+# lane transpositions through LDS for lane bits < WAVE_TR_LDS (default 0:
+# DPP / v_permlane*_swap for all; through LDS measured slower, 0.139 ->
+# 0.146-0.163 ms / gate for lane bits 0 / 0-1 / 0-3, profiles/r3/tr_lds_ab.txt)
+TR_LDS = int(_os.environ.get("WAVE_TR_LDS", "0"))
 
 
 # op record fields live in s[36:59] (prefetch buffer) and s[68:91] (the
@@ -287,6 +291,9 @@ class Gen:
             self.CLA = self.C0
             self.nvgpr = D + 6 * P + 4
         self.handlers = {}
+        # real lane bits below this transpose with a slot through LDS
+        # (gen_tr_lds), the others by DPP / v_permlane*_swap
+        self.tr_lds = TR_LDS
         self.hstart = None       # first body line of the handler being generated
         self.swap_tmp = 0        # rotating temporary of swap_vals
         self.lane_ctrl = False   # generating a ctrl-2 (lane controls only) handler
@@ -793,8 +800,64 @@ class Gen:
         self.end_region()
         self.back()
 
+    def gen_tr_lds(self, s, l):
+        """Transpose slot s with real lane bit l through this wave's LDS
+        outbox (no other wave reads it: no barrier).  A lane with bit l clear
+        gives its registers with slot bit s set and takes the partner's with
+        it clear, a lane with the bit set the other way round: each lane
+        writes the half it gives to its own 64-byte slot (exec = the lanes of
+        one kind at a time), then reads the partner's slot into the same
+        registers -- two rounds (re, im) of 64 bytes per lane.  A handful of
+        VALU instructions instead of 80-128 DPP moves and selects."""
+        e = self.e
+        vt, vl = self.vTmp, self.vLane
+        e("s_nop 1")   # VALU write -> LDS read of the same VGPR
+        # chunk k of lane L at k * 1 KiB + 16 L: the 64 lanes of one
+        # ds_*_b128 cover 1 KiB contiguously (no bank conflicts)
+        e(f"s_mul_i32 s97, s3, {self.OUTBOX}")
+        e(f"v_lshlrev_b32_e32 v{vt}, 4, v{vl}")
+        e(f"v_add_u32_e32 v{vt}, s97, v{vt}")
+        clear = 0
+        for lane in range(64):
+            if not (lane >> l) & 1:
+                clear |= 1 << lane
+        e(f"s_mov_b32 s96, {clear & 0xffffffff:#x}")
+        e(f"s_mov_b32 s97, {clear >> 32:#x}")
+        js = [j for j in range(self.NS) if not (j >> s) & 1]
+        per = 4 // self.P                    # values per 16-byte LDS move
+        for base in (self.re, self.im):
+            # register blocks: consecutive j (bit s clear) with their f = j | 2^s
+            blocks = []
+            for k in range(0, len(js), per):
+                grp = js[k:k + per]
+                assert grp == list(range(grp[0], grp[0] + per)), "TR via LDS: registers not adjacent"
+                blocks.append((base(grp[0]), base(grp[0] | (1 << s))))
+            assert len(blocks) * 16 <= 64
+            for phase in ("w", "r"):
+                if phase == "r":
+                    e("s_waitcnt lgkmcnt(0)")
+                    e(f"v_xor_b32_e32 v{vt}, {16 << l}, v{vt}")     # the partner's slot
+                for kind in ("clear", "set"):
+                    e("s_mov_b64 exec, s[96:97]" if kind == "clear" else "s_not_b64 exec, s[96:97]")
+                    for k, (jr, fr) in enumerate(blocks):
+                        r = fr if kind == "clear" else jr
+                        if phase == "w":
+                            e(f"ds_write_b128 v{vt}, v[{r}:{r + 3}] offset:{1024 * k}")
+                        else:
+                            e(f"ds_read_b128 v[{r}:{r + 3}], v{vt} offset:{1024 * k}")
+                e("s_mov_b64 exec, -1")
+                if phase == "r":
+                    e(f"v_xor_b32_e32 v{vt}, {16 << l}, v{vt}")     # back to ours
+            e("s_waitcnt lgkmcnt(0)")
+        self.back()
+
     def gen_tr(self, s, l):
         self.handler(idx_tr(s, l), f"TR_s{s}_l{l}")
+        # (16-byte LDS moves need 16 bytes of adjacent registers with slot
+        # bit s clear: s >= the vector bits, the only slots the planner moves)
+        if l < self.tr_lds and s >= self.VB:
+            self.gen_tr_lds(s, l)
+            return
         e = self.e
         e("s_nop 1")  # VALU write -> DPP / permlane read of the same VGPR
         pairs = []
@@ -1314,7 +1377,7 @@ class Gen:
         L.append("\t.section\t.rodata,\"a\",@progbits")
         L.append("\t.p2align\t6, 0x0")
         L.append("\t.amdhsa_kernel qa_wave_tile")
-        lds = self.NW * self.OUTBOX if self.W else 0
+        lds = self.NW * self.OUTBOX if (self.W or self.tr_lds) else 0
         for k, v in [("group_segment_fixed_size", lds), ("private_segment_fixed_size", 0), ("kernarg_size", 24),
                      ("user_sgpr_count", 2), ("user_sgpr_dispatch_ptr", 0), ("user_sgpr_queue_ptr", 0),
                      ("user_sgpr_kernarg_segment_ptr", 1), ("user_sgpr_dispatch_id", 0),
