@@ -652,6 +652,16 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 for (int x = 0; x < L; x++) out.perm[x] = pi[out.perm[x]];
             }
         }
+        if (relabelFrom >= 0 && (int)best.size() >= 2 && hooks && hooks->lowPerm) {
+            TilePass& last = out.passes.back();
+            int sigma[64];
+            if (hooks->lowPerm(last, out.ops.data() + last.opBegin, c, sigma)) {
+                for (int i = 0; i < last.k; i++) last.stPos[i] = sigma[last.stPos[i]];
+                while (first < n && done[first]) first++;
+                applyPerm(ops, done, first, sigma);
+                for (int x = 0; x < L; x++) out.perm[x] = sigma[out.perm[x]];
+            }
+        }
         if (ready) hooks->passReady(out, (int)out.passes.size() - 1, order);
     }
     ops.swap(order);

@@ -154,6 +154,12 @@ int& planMaxOps();
 struct PlanHooks {
     std::function<bool(const TilePass&, const TileOp*)> relabelOk;
     std::function<void(const TileProgram&, int pass, const std::vector<Op>& order)> passReady;
+    // lowPerm (relabelling plans): a permutation sigma of the always-resident
+    // positions [relabelFrom, cmin) to compose with the pass's store layout
+    // (every later tile holds all of them, so their order does not change the
+    // plan) -- the wave engine picks the one that spares it transpositions at
+    // the store.  Returns false to keep the layout.
+    std::function<bool(const TilePass&, const TileOp*, int cmin, int* sigma)> lowPerm;
 };
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,

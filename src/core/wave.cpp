@@ -198,6 +198,60 @@ bool waveStoresInPlace(const WavePass& wp) {
     return true;
 }
 
+bool waveLowPerm(const TilePass& ps, const TileOp* ops, int cmin, int* sigma) {
+    static const bool on = !getenv("QUEST_WAVE_LOW_PERM") || atoi(getenv("QUEST_WAVE_LOW_PERM")) != 0;
+    for (int p = 0; p < 64; p++) sigma[p] = p;
+    if (!on || ps.k != kWaveBits) return false;
+    const Stats keep = stats();
+    const long long keepTr = g_waveStoreTrCost;
+    WaveProgram tmp;
+    int endLanes[3];
+    const bool ok = planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp, endLanes);
+    stats() = keep;
+    g_waveStoreTrCost = keepTr;
+    if (!ok) return false;
+    constexpr int VB = kWaveVecBits;
+    // tile bits stored to the always-resident positions [VB, cmin)
+    int bitAt[64];
+    for (int p = 0; p < 64; p++) bitAt[p] = -1;
+    for (int b = 0; b < ps.k; b++)
+        if (ps.stPos[b] >= VB && ps.stPos[b] < cmin) bitAt[ps.stPos[b]] = b;
+    for (int p = VB; p < cmin; p++)
+        if (bitAt[p] < 0) return false;   // (a wave tile holds every position below cmin)
+    int newPos[64];
+    for (int b = 0; b < 64; b++) newPos[b] = -1;
+    bool used[64] = {false};
+    for (int l = 0; l < 3 && VB + l < cmin; l++) {
+        const int b = endLanes[l];
+        if (b >= 0 && ps.stPos[b] >= VB && ps.stPos[b] < cmin && newPos[b] < 0) {
+            newPos[b] = VB + l;
+            used[VB + l] = true;
+        }
+    }
+    int next = VB;
+    for (int p = VB; p < cmin; p++) {
+        const int b = bitAt[p];
+        if (newPos[b] >= 0) continue;
+        while (used[next]) next++;
+        newPos[b] = next;
+        used[next] = true;
+    }
+    bool moved = false;
+    for (int p = VB; p < cmin; p++) {
+        sigma[p] = newPos[bitAt[p]];
+        moved = moved || sigma[p] != p;
+    }
+    if (!moved) return false;
+    // the adjusted layout must still lower (it only spares transpositions)
+    TilePass cand = ps;
+    for (int i = 0; i < cand.k; i++) cand.stPos[i] = sigma[cand.stPos[i]];
+    if (!waveLowers(cand, ops)) {
+        for (int p = 0; p < 64; p++) sigma[p] = p;
+        return false;
+    }
+    return true;
+}
+
 int& waveLaneOrder() {
     static int order = getenv("QUEST_WAVE_LANE_ORDER") ? atoi(getenv("QUEST_WAVE_LANE_ORDER")) : 1;
     return order;
@@ -254,7 +308,7 @@ bool waveChannel(const real* m) {
     return m[2 * 5] == m[2 * 10];
 }
 
-bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out) {
+bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out, int* endLanes) {
     if (ps.k != kWaveBits) return false;
     for (int i = 0; i < kWaveVecBits + 3; i++)
         if (ps.pos[i] != i) return false;
@@ -806,6 +860,8 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         emit(w);
     }
     if (!sig.one()) settleScale(out, wp.opBegin, sig.re, sig.im);
+    if (endLanes)
+        for (int l = 0; l < 3; l++) endLanes[l] = lay.laneBit[l];
     // store layout: the tile bits STORED to positions VB..VB+2 on lane bits
     // 0-2 (one 128-byte line per 8 lanes; the vector bits never left their
     // slots); with a relabelling pass these are other bits than at the load

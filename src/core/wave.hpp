@@ -153,7 +153,15 @@ struct WaveProgram {
 // False if the pass cannot run on the wave engine (tile size other than
 // kWaveBits, non-contiguous low bits, Mat4 / DensChan2 ops, too many tile
 // bits above kWaveLanePosMax).
-bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out);
+// endLanes (optional): the tile bits on real lane bits 0-2 after the ops,
+// before the store layout is restored.
+bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& out, int* endLanes = nullptr);
+
+// PlanHooks::lowPerm of wave plans: reorder the tile bits stored to the
+// always-resident positions [kWaveVecBits, cmin) so that those already on
+// lanes 0-2 at the end of the pass are stored to positions 1-3 (fp64) from
+// there -- the store layout then needs no transposition for them.
+bool waveLowPerm(const TilePass& ps, const TileOp* ops, int cmin, int* sigma);
 
 // In-place relabelling passes (planTiles relabelFrom): on by default for
 // wave programs (QUEST_WAVE_RELABEL=0 / tuning "wave_relabel" turn it off).

@@ -407,6 +407,9 @@ void flush(QuregImpl& q) {
     static const bool streamOn = !getenv("QUEST_PLAN_STREAM") || atoi(getenv("QUEST_PLAN_STREAM")) != 0;
     PlanHooks hooks;
     hooks.relabelOk = [](const TilePass& ps, const TileOp* ops) { return waveLowers(ps, ops); };
+    hooks.lowPerm = [](const TilePass& ps, const TileOp* ops, int c, int* sigma) {
+        return waveLowPerm(ps, ops, c, sigma);
+    };
     std::vector<Op> orig;
     if (relabel) orig = q.pending;
     planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminWave : 4, rt().fusion, prog,
