@@ -62,6 +62,7 @@ int g_rank = 0, g_size = 1;
 enum class Mode { Single, Rccl, Ipc, Socket };
 Mode g_mode = Mode::Single;
 bool g_socket = false;          // QUEST_COMM=socket test transport
+bool g_sharedGpu = false;       // QUEST_RCCL_SHARED_GPU=1: RCCL ranks sharing one GPU
 char* g_stage = nullptr;        // pinned staging for the socket transport
 size_t g_stageBytes = 0;
 ncclComm_t g_comm = nullptr;
@@ -219,6 +220,21 @@ void init(int rank, int size) {
         fprintf(stderr, "QuEST: unknown QUEST_COMM=%s (rccl, ipc or socket)\n", mode);
         exit(EXIT_FAILURE);
     }
+    // QUEST_RCCL_SHARED_GPU=1: several ranks on ONE GPU still run RCCL.  RCCL
+    // refuses two ranks on one device of one host ("Duplicate GPU"), so each
+    // rank presents its own host id (NCCL_HOSTID, read when the communicator
+    // is made) and RCCL connects them through its network transport over
+    // loopback.  Every RCCL call of the data path (grouped send / recv of the
+    // pipelined exchange, allreduce, broadcast, allgather) then runs with N
+    // ranks on a one-GPU machine; only the link differs from xGMI.
+    g_sharedGpu = getenv("QUEST_RCCL_SHARED_GPU") && atoi(getenv("QUEST_RCCL_SHARED_GPU")) != 0;
+    if (g_sharedGpu) {
+        char host[64];
+        snprintf(host, sizeof host, "quest-shared-gpu-rank-%d", rank);
+        setenv("NCCL_HOSTID", host, 1);
+        setenv("NCCL_SOCKET_IFNAME", "lo", 0);
+        setenv("NCCL_IB_DISABLE", "1", 0);
+    }
     // RCCL unique id from rank 0; then every rank reports whether its
     // communicator came up.  If any did not, every rank stops with the
     // reason: a job launched for RCCL over xGMI must not quietly continue on
@@ -241,7 +257,8 @@ void init(int rank, int size) {
         boot::allgather(rank, size, &mine, oks.data(), sizeof(int));
         for (int r = 0; r < size; r++) ok = ok && oks[r];
         if (!ok) {
-            why = "ncclCommInitRank failed on a rank (several ranks on one GPU? use QUEST_COMM=ipc)";
+            why = "ncclCommInitRank failed on a rank (several ranks on one GPU? set QUEST_RCCL_SHARED_GPU=1 or use "
+                  "QUEST_COMM=ipc)";
             if (mine) R.commDestroy(g_comm);
             g_comm = nullptr;
         }
@@ -528,7 +545,11 @@ std::string describe() {
     int v = 0;
     if (R.getVersion) R.getVersion(&v);
     char buf[256];
-    snprintf(buf, sizeof buf, "RCCL %d over xGMI (%d ranks, %s)", v, g_size, g_libName.c_str());
+    if (g_sharedGpu)
+        snprintf(buf, sizeof buf, "RCCL %d, ranks sharing one GPU over its network transport (%d ranks, %s, "
+                 "QUEST_RCCL_SHARED_GPU=1)", v, g_size, g_libName.c_str());
+    else
+        snprintf(buf, sizeof buf, "RCCL %d over xGMI (%d ranks, %s)", v, g_size, g_libName.c_str());
     return buf;
 }
 

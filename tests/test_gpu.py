@@ -302,7 +302,8 @@ _DIST = ["random_ops_statevector", "random_ops_density", "measurement_and_collap
 
 
 @pytest.mark.parametrize("transport,ranks,slice_kb", [("ipc", 2, ""), ("ipc", 4, ""), ("ipc", 4, "1"),
-                                                      ("ipc-nopipe", 2, "1"), ("socket", 2, "")])
+                                                      ("ipc-nopipe", 2, "1"), ("socket", 2, ""), ("rccl", 2, ""),
+                                                      ("rccl", 4, "1")])
 @pytest.mark.parametrize("name", _DIST)
 def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, slice_kb):
     """The distributed router with the HIP kernels (pack/unpack, chunk
@@ -311,7 +312,10 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     GPU-to-GPU-buffer through HIP IPC on the communication stream with the
     RCCL transport's event protocol (pack / exchange / unpack overlapped,
     double-buffered); ipc-nopipe runs every exchange on the compute stream
-    (QUEST_EXCHANGE_PIPELINE=0); socket stages through the host.
+    (QUEST_EXCHANGE_PIPELINE=0); socket stages through the host; rccl runs
+    the production RCCL calls (grouped send / recv on the communication
+    stream, allreduce, broadcast) with N ranks on the one GPU
+    (QUEST_RCCL_SHARED_GPU=1: RCCL's network transport over loopback).
     slice_kb=1 splits every swap into many double-buffered slices."""
     import sys
 
@@ -327,6 +331,8 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
              "QUEST_COMM_TIMEOUT": "180"}
     if transport == "ipc-nopipe":
         extra["QUEST_EXCHANGE_PIPELINE"] = "0"
+    if transport == "rccl":
+        extra["QUEST_RCCL_SHARED_GPU"] = "1"
     if slice_kb:
         extra["QUEST_EXCHANGE_SLICE_KB"] = slice_kb
     res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks, env_extra=extra, timeout=200)
@@ -337,7 +343,7 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     with np.load(out, allow_pickle=False) as z:
         got = {k: z[k] for k in z.files}
     assert int(got["_ranks"]) == ranks
-    assert ("IPC" if transport.startswith("ipc") else "socket") in str(got["_transport"])
+    assert {"ipc": "IPC", "socket": "socket", "rccl": "RCCL"}[transport.split("-")[0]] in str(got["_transport"])
     for k, v in want.items():
         if isinstance(v, str):
             assert str(got[k]) == v, k
