@@ -155,12 +155,17 @@ class _Binding:
             f.restype = res
             f.argtypes = args
 
-        # error handler: record, then the wrapper raises
+        # every wrapped function, resolved once (the per-gate call path)
+        self.fns = {name: getattr(lib, name) for name in self.protos}
+        # error handler: record (per thread), then the wrapper raises; the
+        # wrappers test the plain counter `nerr` (cheap) before looking
         self._err = threading.local()
+        self.nerr = 0
         HANDLER = C.CFUNCTYPE(None, C.c_int, C.c_char_p, C.c_char_p)
 
         def _handler(code, msg, func):
             self._err.value = (int(code), msg.decode(), func.decode())
+            self.nerr += 1
 
         self._handler = HANDLER(_handler)  # keep alive
         self._null_handler = HANDLER()
@@ -202,9 +207,12 @@ class _Binding:
         return a, a.ctypes.data_as(C.POINTER(self.qreal))
 
     def check(self):
+        if not self.nerr:
+            return
         e = getattr(self._err, "value", None)
         if e is not None:
             self._err.value = None
+            self.nerr -= 1
             raise QuESTError(*e)
 
 
@@ -225,9 +233,10 @@ def reset_binding():
 
 
 def _call(name: str, *args):
-    b = binding()
-    res = getattr(b.lib, name)(*args)
-    b.check()
+    b = _binding if _binding is not None else binding()
+    res = b.fns[name](*args) if name in b.fns else getattr(b.lib, name)(*args)
+    if b.nerr:
+        b.check()
     return res
 
 
@@ -264,9 +273,20 @@ def _gen_wrappers():
         "init_genrand", "setGateFusion", "getGateFusion", "setFusionMaxQubits", "flushQureg", "syncQureg",
         "copyStateToGPU", "copyStateFromGPU", "canonicaliseQureg", "resetQuESTStats",
     ]
+    def wrap(name):
+        # the per-gate path: no conversions, one dict lookup, the counter test
+        def w(*a):
+            b = _binding if _binding is not None else binding()
+            res = b.fns[name](*a)
+            if b.nerr:
+                b.check()
+            return res
+
+        w.__name__ = name
+        return w
+
     for n in simple:
-        g[n] = (lambda name: (lambda *a: _call(name, *a)))(n)
-        g[n].__name__ = n
+        g[n] = wrap(n)
     return g
 
 

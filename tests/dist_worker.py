@@ -8,6 +8,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    if os.environ.get("QUEST_TEST_STACKS"):
+        # debugging a hung rank: every thread's Python stack after N seconds
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["QUEST_TEST_STACKS"]), exit=True)
     import quest_amd as qa
     from scenarios import SCENARIOS
 

@@ -332,7 +332,8 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     if transport == "ipc-nopipe":
         extra["QUEST_EXCHANGE_PIPELINE"] = "0"
     if transport == "rccl":
-        extra["QUEST_RCCL_SHARED_GPU"] = "1"
+        # a rank that hangs dumps its Python stack and exits (QUEST_TEST_STACKS)
+        extra.update(QUEST_RCCL_SHARED_GPU="1", QUEST_COMM_TIMEOUT="60", QUEST_TEST_STACKS="120")
     if slice_kb:
         extra["QUEST_EXCHANGE_SLICE_KB"] = slice_kb
     res = spawn_local([os.path.join(here, "dist_worker.py"), name, out], ranks, env_extra=extra, timeout=200)
