@@ -12,6 +12,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -62,6 +63,13 @@ static void readAll(int fd, void* buf, size_t n) {
     }
 }
 
+static bool selfConnected(int fd) {
+    sockaddr_in a{}, b{};
+    socklen_t la = sizeof a, lb = sizeof b;
+    if (getsockname(fd, (sockaddr*)&a, &la) != 0 || getpeername(fd, (sockaddr*)&b, &lb) != 0) return false;
+    return a.sin_port == b.sin_port && a.sin_addr.s_addr == b.sin_addr.s_addr;
+}
+
 static double timeoutSeconds() {
     if (const char* t = getenv("QUEST_BOOTSTRAP_TIMEOUT")) return atof(t);
     return 300.0;
@@ -91,7 +99,12 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
         sa.sin_family = AF_INET;
         sa.sin_port = htons((uint16_t)port);
         sa.sin_addr.s_addr = htonl(INADDR_ANY);
-        if (bind(ls, (sockaddr*)&sa, sizeof sa) != 0) fatal("bind (is QUEST_BOOTSTRAP_PORT free?)");
+        // a peer's connect loop can hold the port for a moment (see the
+        // self-connect note below): retry the bind for a few seconds
+        for (int tries = 0; bind(ls, (sockaddr*)&sa, sizeof sa) != 0; tries++) {
+            if (errno != EADDRINUSE || tries >= 250) fatal("bind (is QUEST_BOOTSTRAP_PORT free?)");
+            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        }
         if (listen(ls, size) != 0) fatal("listen");
         std::vector<int> fds(size, -1);
         for (int k = 1; k < size; k++) {
@@ -121,7 +134,11 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
     int fd = -1;
     while (true) {
         fd = socket(AF_INET, SOCK_STREAM, 0);
-        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+        // A TCP connect to a local port nobody listens on yet can pick that
+        // same port as its ephemeral source and "succeed" against itself
+        // (simultaneous open): rank 0 then cannot bind the port and this rank
+        // waits forever on its own socket.  Drop such a connection and retry.
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd)) break;
         close(fd);
         double waited =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

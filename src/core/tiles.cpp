@@ -663,6 +663,14 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             }
         }
         if (ready) hooks->passReady(out, (int)out.passes.size() - 1, order);
+        if (hooks && hooks->maxPasses > 0 && (int)out.passes.size() >= hooks->maxPasses && (int)order.size() < n) {
+            if (hooks->leftover) {
+                hooks->leftover->clear();
+                for (int i = first; i < n; i++)
+                    if (!done[i]) hooks->leftover->push_back(ops[i]);
+            }
+            break;
+        }
     }
     ops.swap(order);
 }

@@ -160,6 +160,13 @@ struct PlanHooks {
     // plan) -- the wave engine picks the one that spares it transpositions at
     // the store.  Returns false to keep the layout.
     std::function<bool(const TilePass&, const TileOp*, int cmin, int* sigma)> lowPerm;
+    // maxPasses > 0: stop after that many passes (a front flush: the pass is
+    // planned with the whole queue as lookahead, the rest waits for more ops).
+    // The ops not planned go to *leftover, in queue order, already in the
+    // layout the planned passes leave (out.perm applied); `ops` then holds only
+    // the planned ones.
+    int maxPasses = 0;
+    std::vector<Op>* leftover = nullptr;
 };
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,

@@ -369,6 +369,10 @@ void freeComm(void* p) { free(p); }
 
 // ops queued before a flush: the HIP backend's 1024 (QUEST_QUEUE_OPS), so
 // that the emulated wave plans are the GPU's
+namespace {
+void flushImpl(QuregImpl& q, bool front);
+}  // namespace
+
 void enqueue(QuregImpl& q, const Op& op) {
     static const size_t limit = [] {
         const char* e = getenv("QUEST_QUEUE_OPS");
@@ -376,10 +380,23 @@ void enqueue(QuregImpl& q, const Op& op) {
         return (size_t)std::max(1L, std::min(v, 1024L));
     }();
     q.pending.push_back(op);
-    if (q.pending.size() >= limit) flush(q);
+    if (q.pending.size() >= limit) {
+        flush(q);
+        return;
+    }
+    // front flushes of the wave planner, exactly as the HIP backend's
+    // (QUEST_FRONT_FLUSH, default 512 ops): the emulated plans stay the GPU's
+    static const size_t front = [] {
+        const char* e = getenv("QUEST_FRONT_FLUSH");
+        return (size_t)std::max(0L, e ? atol(e) : 512L);
+    }();
+    if (front && q.pending.size() >= front && ((q.pending.size() - front) & 15) == 0) flushImpl(q, true);
 }
 
-void flush(QuregImpl& q) {
+void flush(QuregImpl& q) { flushImpl(q, false); }
+
+namespace {
+void flushImpl(QuregImpl& q, bool front) {
     if (q.pending.empty()) return;
     stats().flushes++;
     const double tFlush0 = trace::on() ? trace::now() : 0.0;
@@ -410,11 +427,20 @@ void flush(QuregImpl& q) {
     hooks.lowPerm = [](const TilePass& ps, const TileOp* ops, int c, int* sigma) {
         return waveLowPerm(ps, ops, c, sigma);
     };
+    std::vector<Op> leftover;
+    if (front) {
+        // as the HIP backend: plain wave queues of wave-sized registers only
+        bool plain = relabel && streamOn && q.L >= kWaveBits + 6;
+        for (const Op& op : q.pending) plain = plain && (op.kind == OpKind::Mat2 || op.kind == OpKind::Diag);
+        if (!plain) return;
+        hooks.maxPasses = 1;
+        hooks.leftover = &leftover;
+    }
     std::vector<Op> orig;
-    if (relabel) orig = q.pending;
+    if (relabel && !front) orig = q.pending;
     planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminWave : 4, rt().fusion, prog,
               relabel ? kWaveVecBits : -1, relabel && streamOn ? &hooks : nullptr);
-    if (relabel && programRelabels(prog) && !relabelsLower(prog)) {
+    if (!front && relabel && programRelabels(prog) && !relabelsLower(prog)) {
         q.pending.swap(orig);
         planTiles(q.pending, q.L, kWaveBits, cminWave, rt().fusion, prog);
     }
@@ -425,7 +451,7 @@ void flush(QuregImpl& q) {
         planPhases(prog, -1, regSlots());
     else if (planner == 2)
         planDenseBlocks(prog, -1, regSlots());
-    q.pending.clear();
+    q.pending.swap(leftover);   // front flush: the ops not planned yet; else empty
     // QUEST_PLAN_ONLY=1 (planner studies): plan, count, do not touch the
     // state -- pass counts of large registers in no time (tools/plan_study.py)
     static const bool planOnly = getenv("QUEST_PLAN_ONLY") && atoi(getenv("QUEST_PLAN_ONLY")) != 0;
@@ -465,6 +491,7 @@ void flush(QuregImpl& q) {
     }
     verifyFlush(q.L, raw.size(), prog.passes.size(), diff);
 }
+}  // namespace
 
 void fill(QuregImpl& q, real re, real im) {
     flush(q);

@@ -196,3 +196,59 @@ def test_emulation_orders_waves_like_the_kernel(barrier):
         assert abs(norm - 1) < 1e-11, norm
     else:
         assert abs(norm - 1) > 1e-3, norm
+
+
+FRONT = r'''
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import quest_amd as qa
+from quest_amd.models import random_layered
+from quest_amd.ops import capi
+from quest_amd.utils import oracle as O
+n = 20
+e = qa.Env()
+r = qa.Register(e, n)
+r.init_plus()
+c = random_layered(n, 36, seed=int(sys.argv[2]))
+capi.resetQuESTStats()
+c.apply(r)
+r.sync()
+st = capi.getQuESTStats()
+o = O.StateVector(n, np.full(1 << n, 2 ** (-n / 2)))
+c.apply_oracle(o)
+err = np.abs(r.to_numpy() - o.v).max()
+print("front gates %d flushes %d passes %d err %.3e" % (len(c.gates), st["flushes"], st["passes"], err))
+assert err < 1e-10, err
+'''
+
+
+def _front(backend, seed, front):
+    env = {"QUEST_BACKEND": backend, "QUEST_FRONT_FLUSH": front}
+    if backend == "cpu":
+        env["QUEST_CPU_PLANNER"] = "3"
+    out = _run(["-c", FRONT, ROOT, str(seed)], env, timeout=600)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    f = out.stdout.split("front")[1].split()
+    return {f[i]: float(f[i + 1]) for i in range(0, len(f), 2)}
+
+
+@pytest.mark.parametrize("front", ["0", "512", "128"])
+def test_front_flush_emulated_on_host(front):
+    """Front flushes (QUEST_FRONT_FLUSH: once that many ops are queued, the
+    first pass is planned with the whole queue as lookahead and runs while
+    the program keeps issuing gates; the rest stays queued in the layout the
+    pass leaves): a 20-qubit, 36-layer circuit (~1100 gates: front flushes,
+    the queue limit and the final sync) on the wave planner's host emulation
+    against the NumPy oracle."""
+    d = _front("cpu", 3, front)
+    if front != "0":
+        assert d["flushes"] > 3, d    # front flushes happened (not just queue-limit + sync)
+
+
+@pytest.mark.gpu
+def test_front_flush_gpu():
+    """The same on the GPU kernel."""
+    for front in ("512", "128"):
+        d = _front("hip", 4, front)
+        assert d["flushes"] > 3, d
