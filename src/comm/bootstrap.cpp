@@ -10,6 +10,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -79,37 +80,67 @@ std::string hostAddress() {
     return envOr("QUEST_BOOTSTRAP_ADDR", "MASTER_ADDR", "127.0.0.1");
 }
 
+// Rank 0's listener, opened at the first rendezvous and kept for the life of
+// the process.  Every rendezvous uses it: a rank connects for rendezvous g + 1
+// only after rank 0 has answered it for g, i.e. after rank 0 accepted every
+// connection of g, so rendezvous never mix.  (Opening a new port per
+// rendezvous collided with RCCL, which listens on ephemeral ports of its own
+// once its communicator exists: a later rendezvous could not bind, and its
+// peers connected to RCCL's listener instead.)
+static int g_listener = -1;
+// rank 0 greets every connection with this word: a rank that reached some
+// other listener on the port (or its own socket) notices and retries
+static const unsigned long long kGreeting = 0x5175455354414d44ull;   // "QuESTAMD"
+
+static bool readGreeting(int fd, double seconds) {
+    timeval tv{};
+    tv.tv_sec = (long)seconds;
+    tv.tv_usec = (long)((seconds - (double)tv.tv_sec) * 1e6);
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    unsigned long long g = 0;
+    size_t got = 0;
+    while (got < sizeof g) {
+        const ssize_t k = ::recv(fd, (char*)&g + got, sizeof g - got, 0);
+        if (k <= 0) return false;
+        got += (size_t)k;
+    }
+    tv = timeval{};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);   // blocking again
+    return g == kGreeting;
+}
+
 void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
     char* out = (char*)all;
     memcpy(out + (size_t)rank * bytes, mine, bytes);
     if (size == 1) return;
 
-    // every rendezvous on its own port (base, base + 1, ...): a rank that
-    // finishes one early must not reach rank 0's previous listener
-    static int generation = 0;
     const std::string addr = hostAddress();
-    const int port = bootstrapPort() + (generation++ % 8);
+    const int port = bootstrapPort();
 
     if (rank == 0) {
-        int ls = socket(AF_INET, SOCK_STREAM, 0);
-        if (ls < 0) fatal("socket");
-        int one = 1;
-        setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-        sockaddr_in sa{};
-        sa.sin_family = AF_INET;
-        sa.sin_port = htons((uint16_t)port);
-        sa.sin_addr.s_addr = htonl(INADDR_ANY);
-        // a peer's connect loop can hold the port for a moment (see the
-        // self-connect note below): retry the bind for a few seconds
-        for (int tries = 0; bind(ls, (sockaddr*)&sa, sizeof sa) != 0; tries++) {
-            if (errno != EADDRINUSE || tries >= 250) fatal("bind (is QUEST_BOOTSTRAP_PORT free?)");
-            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        if (g_listener < 0) {
+            int ls = socket(AF_INET, SOCK_STREAM, 0);
+            if (ls < 0) fatal("socket");
+            int one = 1;
+            setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+            sockaddr_in sa{};
+            sa.sin_family = AF_INET;
+            sa.sin_port = htons((uint16_t)port);
+            sa.sin_addr.s_addr = htonl(INADDR_ANY);
+            // a peer's connect loop can hold the port for a moment (see the
+            // self-connect note below): retry the bind for a few seconds
+            for (int tries = 0; bind(ls, (sockaddr*)&sa, sizeof sa) != 0; tries++) {
+                if (errno != EADDRINUSE || tries >= 250) fatal("bind (is QUEST_BOOTSTRAP_PORT free?)");
+                std::this_thread::sleep_for(std::chrono::milliseconds(20));
+            }
+            if (listen(ls, size) != 0) fatal("listen");
+            g_listener = ls;
         }
-        if (listen(ls, size) != 0) fatal("listen");
         std::vector<int> fds(size, -1);
         for (int k = 1; k < size; k++) {
-            int fd = accept(ls, nullptr, nullptr);
+            int fd = accept(g_listener, nullptr, nullptr);
             if (fd < 0) fatal("accept");
+            writeAll(fd, &kGreeting, sizeof kGreeting);
             int r = -1;
             readAll(fd, &r, sizeof r);
             if (r <= 0 || r >= size || fds[r] >= 0) fatal("bad rank in bootstrap");
@@ -120,11 +151,10 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
             writeAll(fds[r], out, bytes * (size_t)size);
             close(fds[r]);
         }
-        close(ls);
         return;
     }
 
-    // non-root: connect with retries until rank 0 listens
+    // non-root: connect with retries until rank 0 listens and greets
     addrinfo hints{}, *res = nullptr;
     hints.ai_family = AF_INET;
     hints.ai_socktype = SOCK_STREAM;
@@ -137,8 +167,9 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
         // A TCP connect to a local port nobody listens on yet can pick that
         // same port as its ephemeral source and "succeed" against itself
         // (simultaneous open): rank 0 then cannot bind the port and this rank
-        // waits forever on its own socket.  Drop such a connection and retry.
-        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd)) break;
+        // waits forever on its own socket.  Drop such a connection, and one
+        // that does not greet like rank 0, and retry.
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd) && readGreeting(fd, 5.0)) break;
         close(fd);
         double waited =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
