@@ -286,6 +286,57 @@ bool waveLowers(const TilePass& ps, const TileOp* ops) {
     return ok;
 }
 
+// Issue cycles per wave of one op (uncontrolled), from the measured cost of
+// the generated handlers (tools/wave_cost.py over the bench plans, issue
+// costs of profiles/r2/isa_micro_gfx950.txt); slot-controlled ops branch over
+// the registers that fail their controls.
+double waveOpCycles(const WaveOp& w) {
+    double c;
+    switch ((WKind)w.kind) {
+        case WKind::M2: c = 600; break;
+        case WKind::M2R: case WKind::M2RI: case WKind::D2S: c = 300; break;
+        case WKind::ANTI: c = 450; break;
+        case WKind::SWAP: c = 211; break;
+        case WKind::DIAG: c = 256; break;
+        case WKind::D2L: c = 300; break;
+        case WKind::TR: {
+            static const double lane[kWaveLanes] = {517, 563, 341, 339, 264, 259};
+            c = w.b < kWaveLanes ? lane[w.b] : 300;   // wave bits: LDS round trip
+            break;
+        }
+        case WKind::LM2R: c = 724; break;
+        case WKind::LM2RI: c = 578; break;
+        case WKind::LANTI: c = 600; break;
+        case WKind::LSWAP: c = 425; break;
+        case WKind::ROTY: case WKind::ROTX: c = 207; break;
+        case WKind::HADD: c = 140; break;
+        case WKind::YSW: case WKind::YSWC: c = 250; break;
+        case WKind::DROT: c = 190; break;
+        case WKind::DNEG: c = 61; break;
+        case WKind::DMULI: case WKind::DMULNI: c = 236; break;
+        case WKind::DROTN: c = 259; break;
+        default: c = 300; break;   // channels
+    }
+    const bool slotKind = w.kind != (int)WKind::TR && w.kind != (int)WKind::D2L &&
+                          (w.kind < (int)WKind::LM2R || w.kind > (int)WKind::LSWAP);
+    if (slotKind && w.cReg) c *= std::ldexp(1.0, -__builtin_popcount(w.cReg));
+    return c;
+}
+
+double wavePassCycles(const TilePass& ps, const TileOp* ops) {
+    const Stats keep = stats();
+    const long long keepTr = g_waveStoreTrCost;
+    WaveProgram tmp;
+    double c = -1;
+    if (planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp)) {
+        c = 0;
+        for (const WaveOp& w : tmp.ops) c += waveOpCycles(w);
+    }
+    stats() = keep;
+    g_waveStoreTrCost = keepTr;
+    return c;
+}
+
 void applyProgramPerm(QuregImpl& q, const TileProgram& prog) {
     if ((int)prog.perm.size() != q.L) return;
     bool id = true;

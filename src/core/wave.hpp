@@ -173,6 +173,11 @@ bool relabelsLower(const TileProgram& prog);
 // The wave engine can lower this pass (planWavePass on a scratch program; the
 // statistics are left alone): the planner's relabelOk hook.
 bool waveLowers(const TilePass& ps, const TileOp* ops);
+// Estimated issue cycles per wave of one wave op / of a whole tile pass as
+// the wave engine would run it (-1: the pass does not lower) -- the planner's
+// pass-balancing cost (PlanHooks::passCost).
+double waveOpCycles(const WaveOp& w);
+double wavePassCycles(const TilePass& ps, const TileOp* ops);
 // After a program ran: the register's qubits moved by prog.perm.
 void applyProgramPerm(QuregImpl& q, const TileProgram& prog);
 

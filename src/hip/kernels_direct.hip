@@ -72,7 +72,7 @@ __device__ __forceinline__ void forUnits(long long units, F&& f) {
 
 // target >= log2(VN): a vector at `up` (target bit 0) pairs with the vector
 // at up + 2^t.
-template <typename T, int MODE>
+template <typename T, int MODE, bool NT>
 __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                         InsertBits ib, long long tbit, Cm2<T> m) {
     using V = typename Vec16<T>::type;
@@ -86,10 +86,10 @@ __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* _
             const long long u = u0 + k * step;
             up[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
             if (MODE == 2 || up[k] >= 0) {
-                ar[k] = streamLoad(reinterpret_cast<const V*>(re + up[k]));
-                ai[k] = streamLoad(reinterpret_cast<const V*>(im + up[k]));
-                br[k] = streamLoad(reinterpret_cast<const V*>(re + up[k] + tbit));
-                bi[k] = streamLoad(reinterpret_cast<const V*>(im + up[k] + tbit));
+                ar[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(re + up[k]));
+                ai[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(im + up[k]));
+                br[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(re + up[k] + tbit));
+                bi[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(im + up[k] + tbit));
             }
         }
 #pragma unroll
@@ -104,16 +104,16 @@ __global__ __launch_bounds__(256) void mat2DirectKernel(T* __restrict__ re, T* _
                 if ((((unsigned)up[k] + e) & ib.predMask) != ib.predMask) continue;
                 mat2apply(m, pr[e], pi[e], qr[e], qi[e]);
             }
-            streamStore(reinterpret_cast<V*>(re + up[k]), ar[k]);
-            streamStore(reinterpret_cast<V*>(im + up[k]), ai[k]);
-            streamStore(reinterpret_cast<V*>(re + up[k] + tbit), br[k]);
-            streamStore(reinterpret_cast<V*>(im + up[k] + tbit), bi[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(re + up[k]), ar[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(im + up[k]), ai[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(re + up[k] + tbit), br[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(im + up[k] + tbit), bi[k]);
         }
     });
 }
 
 // target inside one vector (bit 0 for fp64, bits 0-1 for fp32)
-template <typename T, int MODE>
+template <typename T, int MODE, bool NT>
 __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                      InsertBits ib, int t, Cm2<T> m) {
     using V = typename Vec16<T>::type;
@@ -127,8 +127,8 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
             const long long u = u0 + k * step;
             at[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
             if (MODE == 2 || at[k] >= 0) {
-                vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
-                vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
+                vr[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(re + at[k]));
+                vi[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(im + at[k]));
             }
         }
 #pragma unroll
@@ -151,8 +151,8 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
                 pairs(std::integral_constant<int, 0>{});
             else
                 pairs(std::integral_constant<int, 1>{});
-            streamStore(reinterpret_cast<V*>(re + at[k]), vr[k]);
-            streamStore(reinterpret_cast<V*>(im + at[k]), vi[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(re + at[k]), vr[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(im + at[k]), vi[k]);
         }
     });
 }
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void mat2LowKernel(T* __restrict__ re, T* __re
 // H at 30 qubits against 7.3 in-vector, tools/direct_ab.py).  Controls
 // below the line are per-element predicates; both halves of a pair agree on
 // them, so a lane that fails keeps its amplitudes.
-template <typename T, int MODE>
+template <typename T, int MODE, bool NT>
 __global__ __launch_bounds__(256) void mat2ShflKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                       InsertBits ib, int t, int lx, Cm2<T> m) {
     using V = typename Vec16<T>::type;
@@ -182,8 +182,8 @@ __global__ __launch_bounds__(256) void mat2ShflKernel(T* __restrict__ re, T* __r
             // 8-lane partner groups are in or out together)
             at[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
             if (MODE == 2 || at[k] >= 0) {
-                vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
-                vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
+                vr[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(re + at[k]));
+                vi[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(im + at[k]));
             } else {
                 vr[k] = V{};
                 vi[k] = V{};
@@ -211,14 +211,14 @@ __global__ __launch_bounds__(256) void mat2ShflKernel(T* __restrict__ re, T* __r
                 pr[e] = ar * x - ai * y + br * qr[e] - bi * qi[e];
                 pi[e] = ar * y + ai * x + br * qi[e] + bi * qr[e];
             }
-            streamStore(reinterpret_cast<V*>(re + at[k]), vr[k]);
-            streamStore(reinterpret_cast<V*>(im + at[k]), vi[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(re + at[k]), vr[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(im + at[k]), vi[k]);
         }
     });
 }
 
 // multiply the amplitudes whose mask bits are all 1
-template <typename T, int MODE>
+template <typename T, int MODE, bool NT>
 __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* __restrict__ im, long long units,
                                                         InsertBits ib, T tr, T ti) {
     using V = typename Vec16<T>::type;
@@ -232,8 +232,8 @@ __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* _
             const long long u = u0 + k * step;
             at[k] = (MODE == 2 || u < units) ? insertAll(u * VN, ib) : -1;
             if (MODE == 2 || at[k] >= 0) {
-                vr[k] = streamLoad(reinterpret_cast<const V*>(re + at[k]));
-                vi[k] = streamLoad(reinterpret_cast<const V*>(im + at[k]));
+                vr[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(re + at[k]));
+                vi[k] = streamLoad<V, NT>(reinterpret_cast<const V*>(im + at[k]));
             }
         }
 #pragma unroll
@@ -248,8 +248,8 @@ __global__ __launch_bounds__(256) void diagDirectKernel(T* __restrict__ re, T* _
                 pr[e] = tr * a - ti * b;
                 pi[e] = tr * b + ti * a;
             }
-            streamStore(reinterpret_cast<V*>(re + at[k]), vr[k]);
-            streamStore(reinterpret_cast<V*>(im + at[k]), vi[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(re + at[k]), vr[k]);
+            streamStore<V, NT>(reinterpret_cast<V*>(im + at[k]), vi[k]);
         }
     });
 }
@@ -279,15 +279,35 @@ int directGrid(long long units, int unr) {
 
 }  // namespace
 
-#define QA_DIRECT_LAUNCH(KER, UNR, ...)                                                                          \
-    do {                                                                                                      \
-        const dim3 grid_(directGrid(units, UNR));                                                              \
-        switch (directMode(units, UNR)) {                                                                      \
-            case 2: hipLaunchKernelGGL((KER<real, 2>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;     \
-            case 1: hipLaunchKernelGGL((KER<real, 1>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;     \
-            default: hipLaunchKernelGGL((KER<real, 0>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;    \
-        }                                                                                                      \
-        QA_HIP_CHECK(hipGetLastError());                                                                       \
+// States of at most QUEST_CACHED_STATE_MB (default 128 MiB, re + im) stay in
+// the 256 MB Infinity Cache from one gate to the next: their kernels use plain
+// loads and stores, larger ones non-temporal accesses (one HBM pass each).
+static bool stateCached(long long amps) {
+    static const long long limit = [] {
+        const char* e = getenv("QUEST_CACHED_STATE_MB");
+        return (e ? atoll(e) : 128ll) << 20;
+    }();
+    return 2ll * (long long)sizeof(real) * amps <= limit;
+}
+
+#define QA_DIRECT_LAUNCH_NT(KER, NT, ...)                                                                          \
+    do {                                                                                                        \
+        switch (directMode(units, 4)) {                                                                          \
+            case 2: hipLaunchKernelGGL((KER<real, 2, NT>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;   \
+            case 1: hipLaunchKernelGGL((KER<real, 1, NT>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;   \
+            default: hipLaunchKernelGGL((KER<real, 0, NT>), grid_, dim3(256), 0, stream(), __VA_ARGS__); break;  \
+        }                                                                                                        \
+    } while (0)
+
+#define QA_DIRECT_LAUNCH(KER, UNR, ...)                                 \
+    do {                                                             \
+        static_assert(UNR == 4, "the direct kernels move 4 units");  \
+        const dim3 grid_(directGrid(units, UNR));                     \
+        if (stateCached(N))                                           \
+            QA_DIRECT_LAUNCH_NT(KER, false, __VA_ARGS__);             \
+        else                                                          \
+            QA_DIRECT_LAUNCH_NT(KER, true, __VA_ARGS__);              \
+        QA_HIP_CHECK(hipGetLastError());                              \
     } while (0)
 
 bool launchDirectOp(real* re, real* im, int L, const Op& op, bool launch) {

@@ -80,28 +80,30 @@ struct NativeVec<float4> {
     using type = qa_nf4;
 };
 
-template <typename V>
+// NT = false: plain accesses (the direct kernels on states that stay in the
+// 256 MB Infinity Cache between gates, hipk::stateCached)
+template <typename V, bool NT = (QA_NONTEMPORAL != 0)>
 __device__ __forceinline__ V streamLoad(const V* p) {
-#if QA_NONTEMPORAL
-    using N = typename NativeVec<V>::type;
-    const N n = __builtin_nontemporal_load(reinterpret_cast<const N*>(p));
-    V v;
-    __builtin_memcpy(&v, &n, sizeof v);
-    return v;
-#else
-    return *p;
-#endif
+    if constexpr (NT) {
+        using N = typename NativeVec<V>::type;
+        const N n = __builtin_nontemporal_load(reinterpret_cast<const N*>(p));
+        V v;
+        __builtin_memcpy(&v, &n, sizeof v);
+        return v;
+    } else {
+        return *p;
+    }
 }
-template <typename V>
+template <typename V, bool NT = (QA_NONTEMPORAL != 0)>
 __device__ __forceinline__ void streamStore(V* p, V v) {
-#if QA_NONTEMPORAL
-    using N = typename NativeVec<V>::type;
-    N n;
-    __builtin_memcpy(&n, &v, sizeof n);
-    __builtin_nontemporal_store(n, reinterpret_cast<N*>(p));
-#else
-    *p = v;
-#endif
+    if constexpr (NT) {
+        using N = typename NativeVec<V>::type;
+        N n;
+        __builtin_memcpy(&n, &v, sizeof n);
+        __builtin_nontemporal_store(n, reinterpret_cast<N*>(p));
+    } else {
+        *p = v;
+    }
 }
 
 #endif  // __HIPCC__
