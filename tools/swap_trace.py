@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Overlap of the distributed swap pipeline from a rocprofv3 kernel +
 memory-copy trace (tools/swap_trace.sh): per process, the pack / unpack
-kernels (packBitsKernel) and the exchange copies, grouped into swaps (gaps
+kernels (packBitsKernel) and the exchange copies (IPC copy kernel, or RCCL's
+kernels), grouped into swaps (gaps
 of > 2 ms between consecutive pack/copy events split swaps); for each swap
 its span, the busy time of pack/unpack and of the copies, and how much of
 the copy time ran concurrently with a pack/unpack kernel.
@@ -70,9 +71,10 @@ def main():
             if "DEVICE_TO_DEVICE" in r.get("Direction", "").upper():
                 per[(f.replace("memory_copy", "kernel"), r.get("Process_Id", "0"))]["c"].append(r)
     # IPC pulls by the library's copy kernel (QUEST_IPC_BLIT=0, the default)
+    # and RCCL's send / recv kernels (QUEST_COMM=rccl)
     for f in kfiles:
         for r in csv.DictReader(open(f)):
-            if "copyVecKernel" in r["Kernel_Name"]:
+            if "copyVecKernel" in r["Kernel_Name"] or "nccl" in r["Kernel_Name"].lower():
                 per[(f, r.get("Process_Id", "0"))]["c"].append(r)
     for (f, pid), v in sorted(per.items()):
         ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "k") for r in v["k"]] + \
