@@ -465,9 +465,8 @@ void barrier() {
 // One-rank RCCL communicator driven through the production code paths: the
 // pipelined exchange (communication stream, ready / done events, double
 // buffering, grouped send + recv -- to itself), the staged scalar allreduce
-// and broadcast, allgather and the async-error watchdog.  A single-GPU
-// machine cannot run two RCCL ranks, so this is how those calls execute on
-// hardware before a multi-GPU job does.
+// and broadcast, allgather and the async-error watchdog, in one process
+// (several ranks on one GPU: QUEST_RCCL_SHARED_GPU=1 in comm::init).
 bool selfTest(std::string& report) {
     char msg[512];
     if (g_size != 1 || g_mode != Mode::Single) {

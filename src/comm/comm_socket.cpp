@@ -2,7 +2,7 @@
 // buffers.  The CPU build's only transport (comm_host.cpp), and in the HIP
 // build the test transport selected by QUEST_COMM=socket (comm_rccl.cpp stages
 // device buffers through pinned host memory), which lets several ranks share
-// ONE GPU -- RCCL refuses two ranks on a device -- so the distributed router
+// ONE GPU without RCCL (which needs QUEST_RCCL_SHARED_GPU=1 for that) -- so the distributed router
 // and its GPU kernels are tested on a single-GPU box (the analogue of the
 // reference's oversubscribed `mpiexec -n 4` runs).
 #include "comm.hpp"
