@@ -196,6 +196,11 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     }
     comm::exchangeWait((int)((nSlices - 1) & 1));
     unpack(nSlices - 1);
+    char moved[128];
+    int at = 0;
+    moved[0] = 0;
+    for (int m = 0; m < k && at < 100; m++)
+        at += snprintf(moved + at, sizeof moved - (size_t)at, "%s[%d, %d]", m ? ", " : "", q.p2l[gpos[m]], q.p2l[lpos[m]]);
     for (int m = 0; m < k; m++) {
         const int g = gpos[m], l = lpos[m];
         const int lg = q.p2l[g], ll = q.p2l[l];
@@ -206,8 +211,8 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     }
     stats().swaps += k;
     if (trace::on())
-        trace::event("swap", "\"k\": %d, \"bytes_sent\": %lld, \"host_ms\": %.3f", k,
-                     stats().bytesExchanged - bytes0, 1e3 * (trace::now() - t0));
+        trace::event("swap", "\"k\": %d, \"bytes_sent\": %lld, \"host_ms\": %.3f, \"in_out\": [%s]", k,
+                     stats().bytesExchanged - bytes0, 1e3 * (trace::now() - t0), moved);
 }
 
 u64 logicalTargets(const Op& op) {
@@ -316,6 +321,11 @@ void restoreChunks(QuregImpl& q) {
 // displacing the local qubits whose first use lies furthest ahead (Belady),
 // as long as that is later than the incoming qubit's.
 void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
+    // run what the backend holds first: its passes may relabel local qubits
+    // (wave relabelling), and the positions chosen below must be the ones the
+    // swap moves (multiSwap's own flush would otherwise move whatever qubit a
+    // relabel put at the victim's old position -- a needless later swap)
+    be::flush(q);
     const int INF = 1 << 30;
     int first[64];
     for (int i = 0; i < 64; i++) first[i] = INF;

@@ -132,3 +132,34 @@ def test_bench_under_torchrun_host_build():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 4 and d["config"]["qubits"] == 16
     assert d["config"]["swaps"] > 0 and d["config"]["norm_error"] < 1e-10
+
+
+def test_swap_victims_survive_relabelling():
+    """The bench window at 2 ranks x 28 qubits with the wave planner's
+    relabelling passes (host emulation, plans only): ONE swap brings the rank
+    qubit in.  Until round 3 the router chose the victim's physical position
+    before flushing the backend, whose relabelling passes then put another
+    qubit there: the swap moved a qubit the rest of the window still needed
+    and a second full swap followed (2 instead of 1 per window at 2 ranks, 3
+    instead of 1 at 8 ranks on the GPU)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, QUEST_BACKEND="cpu", QUEST_CPU_PLANNER="3", QUEST_PLAN_ONLY="1", OMP_NUM_THREADS="2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "QUEST_BOOTSTRAP_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--qubits", "28", "--steps", "20",
+           "--warmup", "5", "--allow-transport", "--no-extras"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["config"]["qubits"] == 29
+    assert d["config"]["swaps"] == 1, d["config"]
