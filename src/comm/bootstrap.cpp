@@ -44,6 +44,30 @@ static void fatal(const char* what) {
     exit(EXIT_FAILURE);
 }
 
+// Non-fatal forms for rank 0's accept loop: a peer that gave up on an earlier
+// connection (greeting timeout) leaves a dead socket in the backlog.
+static bool tryWriteAll(int fd, const void* buf, size_t n) {
+    const char* p = (const char*)buf;
+    while (n) {
+        ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+        if (k <= 0) return false;
+        p += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+static bool tryReadAll(int fd, void* buf, size_t n) {
+    char* p = (char*)buf;
+    while (n) {
+        ssize_t k = ::recv(fd, p, n, 0);
+        if (k <= 0) return false;
+        p += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
 static void writeAll(int fd, const void* buf, size_t n) {
     const char* p = (const char*)buf;
     while (n) {
@@ -137,15 +161,18 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
             g_listener = ls;
         }
         std::vector<int> fds(size, -1);
-        for (int k = 1; k < size; k++) {
+        for (int k = 1; k < size;) {
             int fd = accept(g_listener, nullptr, nullptr);
             if (fd < 0) fatal("accept");
-            writeAll(fd, &kGreeting, sizeof kGreeting);
             int r = -1;
-            readAll(fd, &r, sizeof r);
+            if (!tryWriteAll(fd, &kGreeting, sizeof kGreeting) || !tryReadAll(fd, &r, sizeof r)) {
+                close(fd);   // a connection its rank abandoned; the rank retries
+                continue;
+            }
             if (r <= 0 || r >= size || fds[r] >= 0) fatal("bad rank in bootstrap");
             readAll(fd, out + (size_t)r * bytes, bytes);
             fds[r] = fd;
+            k++;
         }
         for (int r = 1; r < size; r++) {
             writeAll(fds[r], out, bytes * (size_t)size);
@@ -169,7 +196,9 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
         // (simultaneous open): rank 0 then cannot bind the port and this rank
         // waits forever on its own socket.  Drop such a connection, and one
         // that does not greet like rank 0, and retry.
-        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd) && readGreeting(fd, 5.0)) break;
+        // (rank 0 greets when it reaches this rendezvous: wait long enough for
+        // a rank 0 still busy with device or RCCL initialisation)
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd) && readGreeting(fd, 60.0)) break;
         close(fd);
         double waited =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
