@@ -199,7 +199,12 @@ bool waveStoresInPlace(const WavePass& wp) {
 }
 
 bool waveLowPerm(const TilePass& ps, const TileOp* ops, int cmin, int* sigma) {
-    static const bool on = !getenv("QUEST_WAVE_LOW_PERM") || atoi(getenv("QUEST_WAVE_LOW_PERM")) != 0;
+    // on by default for the fp32 tile (5 slots x 3 wave bits); off for the fp64
+    // tile of 5 slots x 2 wave bits, whose plans it made worse on one of five
+    // circuit seeds (15 -> 20 passes; same passes and 0.7 % faster without it,
+    // profiles/r3/wave_shape_variants.txt)
+    static const bool on = getenv("QUEST_WAVE_LOW_PERM") ? atoi(getenv("QUEST_WAVE_LOW_PERM")) != 0
+                                                          : !(kWaveSlots == 5 && kWaveWBits == 2);
     for (int p = 0; p < 64; p++) sigma[p] = p;
     if (!on || ps.k != kWaveBits) return false;
     const Stats keep = stats();

@@ -32,10 +32,11 @@
 
 namespace qa {
 
-// Register slots: 2^4 fp64 / 2^5 fp32 amplitudes per lane (the same 64
-// VGPRs of tile); QA_WAVE_SLOTS_F64 / _F32 override (make WAVE_SLOTS=...)
+// Register slots: 2^5 amplitudes per lane for fp64 (128 VGPRs of tile, four
+// waves per tile) and fp32 (64 VGPRs, eight waves); QA_WAVE_SLOTS_F64 / _F32
+// and QA_WAVE_WBITS_F64 / _F32 override (make WAVE_SLOTS=... WAVE_WBITS=...)
 #ifndef QA_WAVE_SLOTS_F64
-#define QA_WAVE_SLOTS_F64 4
+#define QA_WAVE_SLOTS_F64 5
 #endif
 #ifndef QA_WAVE_SLOTS_F32
 #define QA_WAVE_SLOTS_F32 5
@@ -51,11 +52,19 @@ constexpr int kWaveVecBits = sizeof(real) == 8 ? 1 : 2;
 constexpr int kWaveLanes = 6;   // 64 lanes
 // A tile is shared by 2^kWaveWBits waves of a workgroup: "wave bits" are
 // virtual lane bits 6.. of the tile (transpositions with a slot go through
-// LDS, controls on them are wave-uniform predicates)
-#ifndef QA_WAVE_WBITS
-#define QA_WAVE_WBITS 3
+// LDS, controls on them are wave-uniform predicates).  fp64: 5 slots x 2 wave
+// bits (profiles/r3/wave_shape_variants.txt; round 2-3 before: 4 x 3)
+#ifndef QA_WAVE_WBITS_F64
+#define QA_WAVE_WBITS_F64 2
 #endif
-constexpr int kWaveWBits = QA_WAVE_WBITS;
+#ifndef QA_WAVE_WBITS_F32
+#define QA_WAVE_WBITS_F32 3
+#endif
+#if QuEST_PREC == 1
+constexpr int kWaveWBits = QA_WAVE_WBITS_F32;
+#else
+constexpr int kWaveWBits = QA_WAVE_WBITS_F64;
+#endif
 constexpr int kWaveLaneBits = kWaveLanes + kWaveWBits;  // real + wave lane bits
 constexpr int kWaveBits = kWaveSlots + kWaveLaneBits;
 // real lane bits carry positions up to this (32-bit per-lane byte offsets)
