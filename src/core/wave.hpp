@@ -46,6 +46,8 @@ constexpr int kWaveSlots = QA_WAVE_SLOTS_F32;
 #else
 constexpr int kWaveSlots = QA_WAVE_SLOTS_F64;
 #endif
+// the kernel's register-control masks hold one bit per register in 32 bits
+static_assert(kWaveSlots <= 5, "at most 2^5 registers per lane (32-bit register masks)");
 // tile bits inside one 16-byte vector (they stay in slots 0.. for the whole
 // pass): fp64 tile bit 0, fp32 tile bits 0-1
 constexpr int kWaveVecBits = sizeof(real) == 8 ? 1 : 2;
