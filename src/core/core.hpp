@@ -91,6 +91,9 @@ struct QuregImpl {
     double normCache = 0;
     real* hostRe = nullptr;   // optional host mirror (Qureg.stateVec)
     real* hostIm = nullptr;
+    // wave planner: always-resident low positions chosen for the ops queued
+    // now (chooseWaveCmin), kept until the queue has drained (-1: not chosen)
+    int waveCmin = -1;
     bool permIdentity() const {
         for (int i = 0; i < nSV; i++)
             if (l2p[i] != i) return false;

@@ -342,6 +342,41 @@ double wavePassCycles(const TilePass& ps, const TileOp* ops) {
     return c;
 }
 
+int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks) {
+    // off by default: the two trial plans (about 2 ms on the host, before the
+    // window's first pass starts) cost more than the passes saved on four of
+    // five bench seeds (profiles/r3/cmin_search_ab.txt: +0.7..+1.0 %, one seed
+    // -7.5 %); QUEST_WAVE_CMIN_SEARCH=1 turns it on
+    static const bool on = getenv("QUEST_WAVE_CMIN_SEARCH") && atoi(getenv("QUEST_WAVE_CMIN_SEARCH")) != 0;
+    if (!on || q.pending.size() < 64) return cdefault;
+    if (q.waveCmin >= 0) return q.waveCmin;
+    // plan the queue with cdefault and cdefault + 1 always-resident low
+    // positions (plans only: the relabel / low-permutation hooks, nothing
+    // launched) and keep the one with fewer passes; the choice holds until
+    // the queue drains.  Which one wins varies with the circuit: 15-21 vs
+    // 16-20 passes on five bench seeds (profiles/r3/prof_end_r3.txt)
+    PlanHooks trialHooks;
+    trialHooks.relabelOk = hooks.relabelOk;
+    trialHooks.lowPerm = hooks.lowPerm;
+    const Stats keep = stats();
+    const long long keepTr = g_waveStoreTrCost;
+    size_t best = (size_t)-1;
+    int choice = cdefault;
+    for (int c = cdefault; c <= cdefault + 1 && c < kWaveBits - 1; c++) {
+        std::vector<Op> ops = q.pending;
+        TileProgram prog;
+        planTiles(ops, q.L, kWaveBits, c, true, prog, kWaveVecBits, &trialHooks);
+        if (prog.passes.size() < best) {
+            best = prog.passes.size();
+            choice = c;
+        }
+    }
+    stats() = keep;
+    g_waveStoreTrCost = keepTr;
+    q.waveCmin = choice;
+    return choice;
+}
+
 void applyProgramPerm(QuregImpl& q, const TileProgram& prog) {
     if ((int)prog.perm.size() != q.L) return;
     bool id = true;

@@ -189,6 +189,10 @@ bool waveLowers(const TilePass& ps, const TileOp* ops);
 // pass-balancing cost (PlanHooks::passCost).
 double waveOpCycles(const WaveOp& w);
 double wavePassCycles(const TilePass& ps, const TileOp* ops);
+// Always-resident low positions for a relabelling wave plan of q.pending:
+// cdefault or cdefault + 1, whichever plans fewer passes (QUEST_WAVE_CMIN_SEARCH
+// =1; default: cdefault); sticky in q.waveCmin until the queue drains.
+int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks);
 // After a program ran: the register's qubits moved by prog.perm.
 void applyProgramPerm(QuregImpl& q, const TileProgram& prog);
 

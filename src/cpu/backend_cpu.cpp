@@ -438,8 +438,12 @@ void flushImpl(QuregImpl& q, bool front) {
     }
     std::vector<Op> orig;
     if (relabel && !front) orig = q.pending;
-    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminWave : 4, rt().fusion, prog,
+    // as the HIP backend: 6 or 7 always-resident low positions, whichever
+    // plans this queue in fewer passes
+    const int cminUse = (relabel && streamOn && !getenv("QUEST_WAVE_CMIN")) ? chooseWaveCmin(q, cminWave, hooks) : cminWave;
+    planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminUse : 4, rt().fusion, prog,
               relabel ? kWaveVecBits : -1, relabel && streamOn ? &hooks : nullptr);
+    if (leftover.empty()) q.waveCmin = -1;   // the queue drained: choose afresh next time
     if (!front && relabel && programRelabels(prog) && !relabelsLower(prog)) {
         q.pending.swap(orig);
         planTiles(q.pending, q.L, kWaveBits, cminWave, rt().fusion, prog);
