@@ -49,8 +49,18 @@ void setFusionMaxQubits(int numQubits);
  * im arrays when they are 1 GiB or larger, default 8 GiB, taken only when a
  * tenth of the device stays free), QUEST_ALLOC_MODE (0 two allocations, 1
  * joint with QUEST_IM_OFFSET, 2 physically contiguous, 3 mapped address range
- * with QUEST_IM_DIST; experiments).  Any build: QUEST_DEPHASE_DIAG=0 keeps
- * dephasing channels in channel form instead of diagonal ops. */
+ * with QUEST_IM_DIST; experiments), QUEST_CACHED_STATE_MB (states up to this
+ * size, default 128 MiB, use plain instead of non-temporal accesses in the
+ * unfused kernels), QUEST_SYNC_SPIN=1 (spinning host waits), and for several
+ * ranks QUEST_COMM (rccl default, ipc / socket for ranks sharing one GPU) and
+ * QUEST_RCCL_SHARED_GPU=1 (RCCL itself with several ranks on one GPU: a host
+ * id per rank, RCCL's network transport).  Any build: QUEST_DEPHASE_DIAG=0
+ * keeps dephasing channels in channel form instead of diagonal ops;
+ * QUEST_FRONT_FLUSH (queued ops at which the first wave pass is planned and
+ * launched while the program keeps issuing gates, default 512, 0 = off);
+ * QUEST_DIAG_PHASES (lone diagonal gates as phase ops: 0 never, 1 always,
+ * 2 default: queues of at most 4 ops per qubit); QUEST_WAVE_CMIN_SEARCH=1
+ * (per window, 6 or 7 always-resident low positions by trial plans). */
 int setQuESTTuning(const char* key, int value);
 /* Current value of a tuning knob (into *value); returns 1 if the key is known. */
 int getQuESTTuning(const char* key, int* value);
