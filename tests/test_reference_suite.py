@@ -213,3 +213,24 @@ def test_golden_generate_roundtrip(env, tmp_path):
     b = golden.load_suites()["unit/state_vector/gates/hadamard.test"]["cases"]
     for x, y in zip(a, b):
         assert x["expect"]["P"] == pytest.approx(y["expect"]["P"], abs=1e-10)
+
+
+@pytest.mark.gpu
+def test_golden_suite_rccl_two_ranks_one_gpu():
+    """The 773 reference cases over two ranks on the HIP build with RCCL
+    itself (QUEST_RCCL_SHARED_GPU=1: each rank its own RCCL host id, RCCL's
+    network transport between ranks sharing the GPU): every register is split
+    over the ranks, so gates, reductions, measurements and reads go through
+    the RCCL exchange and collectives."""
+    import os
+
+    from quest_amd.parallel import spawn_local
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = spawn_local(["-m", "quest_amd.utils.golden"], 2,
+                      env_extra={"QUEST_BACKEND": "hip", "QUEST_COMM": "rccl", "QUEST_RCCL_SHARED_GPU": "1",
+                                 "QUEST_COMM_TIMEOUT": "60", "PYTHONPATH": root}, timeout=240)
+    for r, p in enumerate(res):
+        assert p.returncode == 0, f"rank {r}:\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    assert " 0 failed" in res[0].stdout
+    assert int(res[0].stdout.strip().split()[-4]) >= 770
