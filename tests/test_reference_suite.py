@@ -216,8 +216,9 @@ def test_golden_generate_roundtrip(env, tmp_path):
 
 
 @pytest.mark.gpu
-def test_golden_suite_rccl_two_ranks_one_gpu():
-    """The 773 reference cases over two ranks on the HIP build with RCCL
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_golden_suite_rccl_ranks_one_gpu(ranks):
+    """The 773 reference cases over 2 / 4 ranks on the HIP build with RCCL
     itself (QUEST_RCCL_SHARED_GPU=1: each rank its own RCCL host id, RCCL's
     network transport between ranks sharing the GPU): every register is split
     over the ranks, so gates, reductions, measurements and reads go through
@@ -227,7 +228,7 @@ def test_golden_suite_rccl_two_ranks_one_gpu():
     from quest_amd.parallel import spawn_local
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = spawn_local(["-m", "quest_amd.utils.golden"], 2,
+    res = spawn_local(["-m", "quest_amd.utils.golden"], ranks,
                       env_extra={"QUEST_BACKEND": "hip", "QUEST_COMM": "rccl", "QUEST_RCCL_SHARED_GPU": "1",
                                  "QUEST_COMM_TIMEOUT": "60", "PYTHONPATH": root}, timeout=240)
     for r, p in enumerate(res):
