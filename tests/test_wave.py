@@ -224,8 +224,8 @@ assert err < 1e-10, err
 '''
 
 
-def _front(backend, seed, front):
-    env = {"QUEST_BACKEND": backend, "QUEST_FRONT_FLUSH": front}
+def _front(backend, seed, front, **extra):
+    env = dict({"QUEST_BACKEND": backend, "QUEST_FRONT_FLUSH": front}, **extra)
     if backend == "cpu":
         env["QUEST_CPU_PLANNER"] = "3"
     out = _run(["-c", FRONT, ROOT, str(seed)], env, timeout=600)
@@ -253,3 +253,10 @@ def test_front_flush_gpu():
     for front in ("512", "128"):
         d = _front("hip", 4, front)
         assert d["flushes"] > 3, d
+
+
+def test_cmin_search_emulated_on_host():
+    """QUEST_WAVE_CMIN_SEARCH=1 (each window planned with 6 or 7 always-resident
+    low positions, whichever gives fewer passes) on the host emulation
+    against the NumPy oracle."""
+    _front("cpu", 5, "512", QUEST_WAVE_CMIN_SEARCH="1")
