@@ -255,6 +255,75 @@ def test_front_flush_gpu():
         assert d["flushes"] > 3, d
 
 
+PHASES = r'''
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import quest_amd as qa
+from quest_amd.models.circuits import Circuit, random_mixed
+from quest_amd.ops import capi
+from quest_amd.utils import oracle as O
+n = 18
+e = qa.Env()
+r = qa.Register(e, n)
+r.init_plus()
+c = random_mixed(n, 480, seed=int(sys.argv[2]), high=6)
+capi.resetQuESTStats()
+# short windows (a read every 24 gates), where QUEST_DIAG_PHASES=2 lowers
+# the diagonal gates to phase ops
+for i in range(0, len(c.gates), 24):
+    part = Circuit(n)
+    part.gates = c.gates[i:i + 24]
+    part.apply(r)
+    r.sync()
+st = capi.getQuESTStats()
+o = O.StateVector(n, np.full(1 << n, 2 ** (-n / 2)))
+c.apply_oracle(o)
+err = np.abs(r.to_numpy() - o.v).max()
+print("phases passes %d err %.3e" % (st["passes"], err))
+assert err < 1e-10, err
+'''
+
+
+def _phases(backend, mode, seed):
+    env = {"QUEST_BACKEND": backend, "QUEST_DIAG_PHASES": mode}
+    if backend == "cpu":
+        env["QUEST_CPU_PLANNER"] = "3"
+    out = _run(["-c", PHASES, ROOT, str(seed)], env, timeout=600)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    return int(out.stdout.split("passes")[1].split()[0])
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_diagonal_gates_as_phases_emulated_on_host(mode):
+    """QUEST_DIAG_PHASES (tiles.cpp phasesFromDiagonals: a unit-modulus
+    diagonal gate -- Z, S, T, Rz, phase shifts, their controlled and
+    multi-controlled forms -- becomes phase ops that need no tile bit): mixed
+    random gates in short windows on the host emulation against the oracle,
+    never, always and for short queues (default)."""
+    passes = _phases("cpu", mode, 11)
+    assert passes > 0
+
+
+@pytest.mark.gpu
+def test_diagonal_gates_as_phases_gpu():
+    """The same on the GPU kernel; lowering never costs passes here."""
+    never, always = _phases("hip", "0", 12), _phases("hip", "1", 12)
+    assert always <= never, (always, never)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"QUEST_CACHED_STATE_MB": "0"}, {"QUEST_CACHED_STATE_MB": "4096"},
+                                 {"QUEST_SYNC_SPIN": "1"}])
+def test_unfused_kernel_variants_gpu(env):
+    """The unfused direct kernels with non-temporal accesses at every size
+    (QUEST_CACHED_STATE_MB=0) and with plain, cache-resident accesses for the
+    whole 18-qubit state (4096), and spinning host waits: mixed random gates
+    against the oracle."""
+    out = _run(["-c", PHASES, ROOT, "13"], dict({"QUEST_BACKEND": "hip", "QUEST_FUSION": "0"}, **env))
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+
+
 def test_cmin_search_emulated_on_host():
     """QUEST_WAVE_CMIN_SEARCH=1 (each window planned with 6 or 7 always-resident
     low positions, whichever gives fewer passes) on the host emulation
