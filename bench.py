@@ -139,7 +139,10 @@ def main():
     s_per_gate = elapsed / max(gates, 1)
     extras = {}
     if world == 1 and not args.no_extras and qa.capi.getQuESTBackend() == "HIP":
-        extras = run_extras(qa, reg, n, layer_gates, args)   # closes reg
+        try:
+            extras = run_extras(qa, reg, n, layer_gates, args)   # closes reg
+        except Exception as e:  # an optional extra must never cost the headline
+            extras = {"extras_error": f"{type(e).__name__}: {e}"[:500]}
         if "s_per_gate" in extras.get("fp32", {}):
             extras["fp32"]["ratio_to_fp64"] = extras["fp32"]["s_per_gate"] / (elapsed / max(gates, 1))
     else:
@@ -199,7 +202,15 @@ def run_extras(qa, reg, n, layer_gates, args):
 
     todo = set(args.extras.split(","))
     out = {}
-    if "window1" in todo:
+
+    def guarded(key, fn):
+        # each extra is optional: its failure is recorded, never raised
+        try:
+            fn()
+        except Exception as e:
+            out[key] = {"error": f"{type(e).__name__}: {e}"[:500]}
+
+    def window1():
         # one-layer window: the same layers, flushed one at a time
         t0 = time.perf_counter()
         g = 0
@@ -209,7 +220,8 @@ def run_extras(qa, reg, n, layer_gates, args):
             g += len(layer_gates[args.warmup + s])
         reg.sync()
         out["window1_s_per_gate"] = (time.perf_counter() - t0) / max(g, 1)
-    if "fork30" in todo:
+
+    def fork30():
         # fork program on a fresh register (the bench register stays allocated)
         fork = fork_circuit()
         f = qa.Register(reg.envobj, 30)
@@ -226,7 +238,8 @@ def run_extras(qa, reg, n, layer_gates, args):
         out["fork30"] = {"total_s": t3 - t0, "gates_s": t1 - t0, "probs_s": t2 - t1, "amps_s": t3 - t2,
                          "gates": len(fork.gates), "p_q0": probs[0], "amp0": [amps[0].real, amps[0].imag]}
         f.close()
-    if "sweep" in todo:
+
+    def sweep_run():
         # unfused single-qubit gate time vs #qubits
         qa.capi.setGateFusion(0)
         sweep = []
@@ -249,18 +262,24 @@ def run_extras(qa, reg, n, layer_gates, args):
             r.close()
         qa.capi.setGateFusion(1)
         out["sweep"] = sweep
+
+    if "window1" in todo:
+        guarded("window1", window1)
+    if "fork30" in todo:
+        guarded("fork30", fork30)
+    if "sweep" in todo:
+        guarded("sweep", sweep_run)
+        qa.capi.setGateFusion(1)
     env = reg.envobj
     reg.close()
     if qa.capi.binding().prec == 2:
         res = {}
         if "q34" in todo:
-            run_q34(env, res)
-            out["q34"] = res["q34"]
+            guarded("q34", lambda: (run_q34(env, res), out.__setitem__("q34", res["q34"])))
         if "density17" in todo:
-            run_density17(env, res)
-            out["density17"] = res["density17"]
+            guarded("density17", lambda: (run_density17(env, res), out.__setitem__("density17", res["density17"])))
     if "fp32" in todo and qa.capi.binding().prec == 2:
-        out["fp32"] = _run_fp32(args)
+        guarded("fp32", lambda: out.__setitem__("fp32", _run_fp32(args)))
     return out
 
 
@@ -274,10 +293,16 @@ def _run_fp32(args):
     env = dict(os.environ, QUEST_PREC="1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "fp32 child timed out after 300 s"}
     if p.returncode != 0:
         return {"error": p.stderr[-500:]}
-    d = json.loads(p.stdout.strip().splitlines()[-1])
+    try:
+        d = json.loads(p.stdout.strip().splitlines()[-1])
+    except (IndexError, ValueError) as e:
+        return {"error": f"fp32 child printed no JSON line: {e}"}
     return {"s_per_gate": d["value"], "passes": d["config"]["passes"], "norm_error": d["config"]["norm_error"],
             "unfused_gate_s": d["config"]["unfused_gate_s"], "dtype": d["dtype"]}
 

@@ -13,12 +13,14 @@
 #include <sys/time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <algorithm>
 #include <string>
 #include <thread>
 #include <vector>
@@ -157,7 +159,9 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
                 if (errno != EADDRINUSE || tries >= 250) fatal("bind (is QUEST_BOOTSTRAP_PORT free?)");
                 std::this_thread::sleep_for(std::chrono::milliseconds(20));
             }
-            if (listen(ls, size) != 0) fatal("listen");
+            // room for connections that ranks abandoned (greeting timeouts)
+            // and retried, so new connects never stall on a full accept queue
+            if (listen(ls, std::max(size * 8, SOMAXCONN)) != 0) fatal("listen");
             g_listener = ls;
         }
         std::vector<int> fds(size, -1);
@@ -198,7 +202,9 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
         // that does not greet like rank 0, and retry.
         // (rank 0 greets when it reaches this rendezvous: wait long enough for
         // a rank 0 still busy with device or RCCL initialisation)
-        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd) && readGreeting(fd, 60.0)) break;
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd) &&
+            readGreeting(fd, std::max(60.0, timeoutSeconds())))
+            break;
         close(fd);
         double waited =
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

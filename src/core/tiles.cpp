@@ -588,6 +588,52 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         }
         return high;
     };
+    // Compute-aware passes (PlanHooks::passCost): drop ops from the end of a
+    // pass predicted to be compute-bound, as long as each dropped op could run
+    // in any later pass at no extra tile bits (a phase, or targets among the
+    // always-resident low positions), no op kept after it in the pass depends
+    // on it, and some op outside the pass remains anyway (there will be a
+    // later pass to take them).
+    auto trimPass = [&](std::vector<int>& v, u64 high) {
+        auto cost = [&](const std::vector<int>& sel) {
+            std::vector<Op> tmp;
+            tmp.reserve(sel.size());
+            for (int i : sel) tmp.push_back(ops[i]);
+            TileProgram scratch;
+            emitPass(tmp, 0, (int)tmp.size(), high, L, k, c, scratch);
+            const TilePass& ps = scratch.passes.back();
+            return hooks->passCost(ps, scratch.ops.data() + ps.opBegin);
+        };
+        const double C = cost(v);
+        const double bound = hooks->memCost * (1 + hooks->costMargin);
+        if (C <= bound) return;
+        // another op stays queued after this pass?
+        std::vector<char> inPass(n, 0);
+        for (int i : v) inPass[i] = 1;
+        bool rest = false;
+        for (int i = first; i < n && !rest; i++) rest = !done[i] && !inPass[i];
+        if (!rest) return;
+        const double perOp = C / (double)v.size();
+        double excess = C - bound;
+        std::vector<char> drop(v.size(), 0);
+        u64 keptTg = 0, keptTouch = 0;   // of the kept ops after the candidate
+        for (int x = (int)v.size() - 1; x >= 0 && excess > 0; x--) {
+            const Op& op = ops[v[(size_t)x]];
+            const u64 tg = targetMask(op), touch = tg | op.ctrl;
+            const bool movable = op.kind == OpKind::Diag || (op.kind == OpKind::Mat2 && !(tg & ~low));
+            if (movable && !(tg & keptTouch) && !(touch & keptTg)) {
+                drop[(size_t)x] = 1;
+                excess -= perOp;
+                continue;
+            }
+            keptTg |= tg;
+            keptTouch |= touch;
+        }
+        std::vector<int> kept;
+        for (size_t x = 0; x < v.size(); x++)
+            if (!drop[x]) kept.push_back(v[x]);
+        if (kept.size() < v.size() && !kept.empty()) v.swap(kept);
+    };
     while ((int)order.size() < n) {
         while (done[first]) first++;
         const int begin = (int)order.size();
@@ -644,6 +690,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 bestScore = sc;
             }
         }
+        if (hooks && hooks->passCost && hooks->memCost > 0 && best.size() > 1) trimPass(best, bestHigh);
         for (int i : best) {
             order.push_back(ops[i]);
             done[i] = 1;

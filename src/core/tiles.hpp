@@ -167,6 +167,16 @@ struct PlanHooks {
     // the planned ones.
     int maxPasses = 0;
     std::vector<Op>* leftover = nullptr;
+    // Compute-aware passes (passCost set, memCost > 0): passCost predicts the
+    // compute of a pass (e.g. wave issue cycles per tile, -1: unknown) and
+    // memCost is the same measure of one pass's memory stream.  A pass whose
+    // predicted compute exceeds memCost * (1 + costMargin) leaves some of its
+    // ops that any later pass can take (phases, targets on always-resident
+    // positions, nothing after them in the pass depending on them) to the
+    // passes after it, which are memory-bound more often than not.
+    std::function<double(const TilePass&, const TileOp*)> passCost;
+    double memCost = 0;
+    double costMargin = 0.1;
 };
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,

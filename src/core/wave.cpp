@@ -194,6 +194,8 @@ bool& waveRelabel() {
 bool waveStoresInPlace(const WavePass& wp) {
     if (wp.stFlipLane >> kWaveLanes) return false;   // wave w stores where wave w ^ f loaded
     for (int l = kWaveLanes; l < kWaveLaneBits; l++)
+        if (wp.stCondLane[l]) return false;          // ... or where a wave-conditioned flip sends it
+    for (int l = kWaveLanes; l < kWaveLaneBits; l++)
         if (wp.pos[wp.ldLane[l]] != wp.stPos[wp.stLane[l]]) return false;
     return true;
 }
@@ -342,6 +344,19 @@ double wavePassCycles(const TilePass& ps, const TileOp* ops) {
     return c;
 }
 
+void waveCostHooks(PlanHooks& hooks) {
+    // One pass's HBM stream in the units of wavePassCycles: a 30-qubit pass
+    // streams in about 5.6 ms, the time the kernel issues about 12800 modeled
+    // cycles per wave and tile (profiles/r3/overlap_study_one_tile_per_wg.txt
+    // against the plan's modeled cycles); both scale with the tile count.
+    static const double mem = getenv("QUEST_PLAN_MEM_CYCLES") ? atof(getenv("QUEST_PLAN_MEM_CYCLES")) : 12800.0;
+    static const double margin = getenv("QUEST_PLAN_COST_MARGIN") ? atof(getenv("QUEST_PLAN_COST_MARGIN")) : 0.1;
+    if (mem <= 0) return;
+    hooks.passCost = [](const TilePass& ps, const TileOp* ops) { return wavePassCycles(ps, ops); };
+    hooks.memCost = mem;
+    hooks.costMargin = margin;
+}
+
 int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks) {
     // off by default: the two trial plans (about 2 ms on the host, before the
     // window's first pass starts) cost more than the passes saved on four of
@@ -414,6 +429,17 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         else if (k != OpKind::Diag)
             return false;
     }
+    // Conditional exchange frame (QUEST_WAVE_CFRAME=0 disables; needs the
+    // exchange frame below): a CNOT with one control inside the tile and no
+    // control outside is not executed either -- its target is marked flipped
+    // where its control is 1 (see Cnd below), so it needs no register slot
+    static const bool cframeOn = (!getenv("QUEST_WAVE_XFRAME") || atoi(getenv("QUEST_WAVE_XFRAME")) != 0) &&
+                                 (!getenv("QUEST_WAVE_CFRAME") || atoi(getenv("QUEST_WAVE_CFRAME")) != 0);
+    auto deferCnot = [&](int i) {
+        const TileOp& op = ops[i];
+        return cframeOn && (OpKind)op.kind == OpKind::Mat2 && cls[i] == M2Class::Swap && op.ctrlOut == 0 &&
+               __builtin_popcount(op.ctrlIn) == 1 && op.t[0] >= kWaveVecBits;
+    };
     // ops that need their target(s) in a register slot
     auto needsSlot = [&](int i) { return (OpKind)ops[i].kind == OpKind::Mat2 && cls[i] != M2Class::Diag; };
     auto slotTargets = [&](int i, int* t) {
@@ -423,7 +449,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             return 2;
         }
         t[0] = ops[i].t[0];
-        return needsSlot(i) ? 1 : 0;
+        return needsSlot(i) && !deferCnot(i) ? 1 : 0;
     };
     // next[i][b]: first op >= i needing tile bit b in a slot
     std::vector<int> nextNeed((size_t)(nOps + 1) * kWaveBits, kInf);
@@ -761,7 +787,147 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         }
         transpose(victim, l);
     };
+    // Conditional flips: tile bit t additionally flipped where the tile bits
+    // in Cnd[t] have odd parity.  With p the physical coordinates of an
+    // amplitude (the bits where each tile bit currently lives), its logical
+    // tile index x has x_t = p_t ^ F_t ^ parity(p & Cnd[t]).  Invariant: a
+    // condition bit has no conditions itself, so the pairs of a gate on a
+    // target t are still the pairs along p_t (t is never a condition) and the
+    // gate only has to be oriented: X M X where the parity is odd.  Deferred
+    // CNOTs are executed (SWAP with the condition as its control) only when an
+    // op needs it; at the end of the pass the flips whose target and
+    // conditions are in one domain (slots, real lanes, wave bits) are folded
+    // into the store maps (WavePass::stCondSlot / stCondLane).
+    unsigned Cnd[kWaveBits] = {0};
+    auto deps = [&](int c) {
+        unsigned m = 0;
+        for (int u = 0; u < kWaveBits; u++) m |= ((Cnd[u] >> c) & 1u) << u;
+        return m;
+    };
+    // ops in physical terms (no frame adjustment): a CNOT c -> t, a Z, a CZ
+    auto rawCnot = [&](int i, int c, int t) {
+        WaveOp x;
+        const int wt = lay.where[t];
+        if (!inSlot(wt) && laneOf(wt) < kWaveLaneOps) {
+            x = blank((int)WKind::LSWAP);
+            x.a = laneOf(wt);
+        } else {
+            if (!inSlot(wt)) toSlot(i, t, inSlot(lay.where[c]) ? lay.where[c] : -1);
+            x = blank((int)WKind::SWAP);
+            x.a = lay.where[t];
+        }
+        masks(lay, 1u << c, x.cReg, x.cLane);
+        out.ops.push_back(x);
+        Cnd[t] &= ~(1u << c);
+    };
+    auto rawZ = [&](unsigned tileMask) {
+        WaveOp z = blank((int)WKind::DNEG);
+        masks(lay, tileMask, z.cReg, z.cLane);
+        out.ops.push_back(z);
+    };
+    auto execConds = [&](int i, int t) {   // execute t's deferred CNOTs
+        for (unsigned m = Cnd[t]; m; m &= m - 1) rawCnot(i, __builtin_ctz(m), t);
+    };
+    auto clean = [&](int i, int c) {          // execute the deferred CNOTs controlled by c
+        for (unsigned m = deps(c); m; m &= m - 1) rawCnot(i, c, __builtin_ctz(m));
+    };
+    auto laneOpPath = [&](int i, int t) {
+        return !inSlot(lay.where[t]) && laneOf(lay.where[t]) < kWaveLaneOps && cls[i] != M2Class::General &&
+               remaining[(size_t)i * kWaveBits + t] <= laneOpsMax(t);
+    };
+    // Resolve the conditional frame before op i: 1 = the op was applied here
+    // (a deferred CNOT, a Z or Y on a conditioned bit); postT / postCZ / postClear:
+    // CZs to emit after the op (orientation by Z M Z, or the Z an H leaves)
+    int postT = -1;
+    unsigned postCZ = 0;
+    bool postClear = false;
+    auto frameBefore = [&](int i) -> int {
+        const TileOp& op = ops[i];
+        postT = -1;
+        postCZ = 0;
+        postClear = false;
+        if (deferCnot(i)) {
+            const int t = op.t[0], k = __builtin_ctz(op.ctrlIn);
+            if (Cnd[k]) execConds(i, k);   // the control must be a plain physical bit
+            if (deps(t)) clean(i, t);       // the target must not condition other bits
+            Cnd[t] ^= 1u << k;
+            F ^= ((F >> k) & 1u) << t;     // x_t ^= x_k = p_k ^ F_k
+            return 1;
+        }
+        if (chan[i]) {
+            for (int b : {op.t[0], op.t[1]}) {
+                execConds(i, b);
+                clean(i, b);
+            }
+            return 0;
+        }
+        for (unsigned m = op.ctrlIn; m; m &= m - 1)
+            if (Cnd[__builtin_ctz(m)]) execConds(i, __builtin_ctz(m));
+        const real* m = op.m;
+        const bool isMat2 = (OpKind)op.kind == OpKind::Mat2;
+        if (!isMat2 || cls[i] == M2Class::Diag) {
+            const unsigned mask = op.ctrlIn | (isMat2 ? 1u << op.t[0] : 0u);
+            // Z on one bit: (-1)^x_t = (-1)^p_t (-1)^F_t prod_c (-1)^p_c
+            int zt = -1;
+            if (op.ctrlOut == 0 && !isMat2 && __builtin_popcount(mask) == 1 && m[0] == -1 && m[1] == 0)
+                zt = __builtin_ctz(mask);
+            if (op.ctrlOut == 0 && isMat2 && op.ctrlIn == 0 && m[0] == 1 && m[1] == 0 && m[6] == -1 && m[7] == 0)
+                zt = op.t[0];
+            if (zt >= 0 && Cnd[zt]) {
+                rawZ(1u << zt);
+                for (unsigned c = Cnd[zt]; c; c &= c - 1) rawZ(1u << __builtin_ctz(c));
+                if ((F >> zt) & 1u) sig.mul(-1, 0);
+                return 1;
+            }
+            for (unsigned b = mask; b; b &= b - 1)
+                if (Cnd[__builtin_ctz(b)]) execConds(i, __builtin_ctz(b));
+            return 0;
+        }
+        const int t = op.t[0];
+        const bool unc = op.ctrlIn == 0 && op.ctrlOut == 0;
+        const bool isY = cls[i] == M2Class::Anti && m[2] == 0 && m[4] == 0 && std::fabs(m[3]) == 1 && m[5] == -m[3];
+        // an uncontrolled X / Y on a condition only toggles F_t (and a Z on p_t)
+        if (deps(t) && !(unc && t >= VB && (cls[i] == M2Class::Swap || isY))) clean(i, t);
+        if (!Cnd[t] || cls[i] == M2Class::Swap) return 0;   // X commutes with the orientation
+        const bool commX = near(m[0], m[6]) && near(m[1], m[7]) && near(m[2], m[4]) && near(m[3], m[5]);
+        const bool zmz = near(m[0], m[6]) && near(m[1], m[7]) && near(m[2], -m[4]) && near(m[3], -m[5]);
+        const bool isH = cheap && unc && cls[i] == M2Class::Real && near(m[0], m[2]) && near(m[0], m[4]) &&
+                         near(m[0], -m[6]);
+        if (commX) return 0;
+        if (unc && isY) {   // Y = i X Z (-Y = -i X Z): Z on x_t, then X into the frame
+            rawZ(1u << t);
+            for (unsigned c = Cnd[t]; c; c &= c - 1) rawZ(1u << __builtin_ctz(c));
+            if ((F >> t) & 1u) sig.mul(-1, 0);
+            F ^= 1u << t;
+            sig.mul(0, m[3] < 0 ? 1 : -1);
+            return 1;
+        }
+        if (zmz) {   // X M X = Z M Z: CZ(c, t) for every condition before and after
+            for (unsigned c = Cnd[t]; c; c &= c - 1) rawZ((1u << __builtin_ctz(c)) | (1u << t));
+            postT = t;
+            postCZ = Cnd[t];
+            return 0;
+        }
+        if (isH && !laneOpPath(i, t)) {   // H X^s = Z^s H: the CZs after clear the conditions
+            postT = t;
+            postCZ = Cnd[t];
+            postClear = true;
+            return 0;
+        }
+        execConds(i, t);
+        return 0;
+    };
+    auto frameAfter = [&]() {
+        if (postT < 0) return;
+        for (unsigned c = postCZ; c; c &= c - 1) rawZ((1u << __builtin_ctz(c)) | (1u << postT));
+        if (postClear) Cnd[postT] = 0;
+        postT = -1;
+    };
     for (int i = 0; i < nOps; i++) {
+        if (cframeOn) {
+            frameAfter();
+            if (frameBefore(i)) continue;
+        }
         const TileOp& op = ops[i];
         if (chan[i]) {
             const int r = op.t[0], c = op.t[1];
@@ -950,6 +1116,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         w.ctrlOut = op.ctrlOut;
         emit(w);
     }
+    if (cframeOn) frameAfter();
     if (!sig.one()) settleScale(out, wp.opBegin, sig.re, sig.im);
     if (endLanes)
         for (int l = 0; l < 3; l++) endLanes[l] = lay.laneBit[l];
@@ -964,28 +1131,72 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // (these transpositions are about 40 % of a pass's weighted transposition
     // cost on the bench circuit, but stores that skip them are not 128-byte
     // coalesced: 0.284 instead of 0.199 ms/gate, same-box A/B)
-    for (int l = 0; l < 3; l++) {
-        const int b = stBit[VB + l];
-        if (b < 0) return false;
-        const int w = lay.where[b];
-        if (w == kWaveSlots + l) continue;
-        if (inSlot(w)) {
-            transpose(w, l);
-        } else {
-            // b sits on another lane bit (>= 3): through the first free slot
-            transpose(VB, laneOf(w));
-            transpose(VB, l);
-        }
-    }
-    // real lane bits 3.. may not carry positions above kWaveLanePosMax at store
+    // the store layout's transpositions on `L2` (real: emitted, L2 is lay;
+    // else only L2 is updated -- a dry run)
     auto farSt = [&](int b) { return ps.stPos[b] > kWaveLanePosMax; };
-    for (int l = 3; l < kWaveLanes; l++) {
-        if (!farSt(lay.laneBit[l])) continue;
-        int s = -1;
-        for (int x = VB; x < kWaveSlots && s < 0; x++)
-            if (!farSt(lay.slotBit[x])) s = x;
-        if (s < 0) return false;  // cannot happen: at most kWaveSlots - 1 far bits
-        transpose(s, l);
+    auto storeLayout = [&](Layout& L2, bool real) -> bool {
+        auto tr = [&](int s, int l) {
+            if (real) {
+                transpose(s, l);
+                return;
+            }
+            const int bs = L2.slotBit[s], bl = L2.laneBit[l];
+            L2.put(bs, kWaveSlots + l);
+            L2.put(bl, s);
+        };
+        for (int l = 0; l < 3; l++) {
+            const int b = stBit[VB + l];
+            if (b < 0) return false;
+            const int w = L2.where[b];
+            if (w == kWaveSlots + l) continue;
+            if (inSlot(w)) {
+                tr(w, l);
+            } else {
+                // b sits on another lane bit (>= 3): through the first free slot
+                tr(VB, laneOf(w));
+                tr(VB, l);
+            }
+        }
+        // real lane bits 3.. may not carry positions above kWaveLanePosMax at store
+        for (int l = 3; l < kWaveLanes; l++) {
+            if (!farSt(L2.laneBit[l])) continue;
+            int s = -1;
+            for (int x = VB; x < kWaveSlots && s < 0; x++)
+                if (!farSt(L2.slotBit[x])) s = x;
+            if (s < 0) return false;  // cannot happen: at most kWaveSlots - 1 far bits
+            tr(s, l);
+        }
+        return true;
+    };
+    // conditional flips left at the end: those whose target and conditions
+    // sit in one domain of the store layout (slots >= VB, real lanes, wave
+    // bits) become store maps; the others are executed now
+    auto domain = [](int w) { return inSlot(w) ? (w >= VB ? 0 : -1) : (laneOf(w) < kWaveLanes ? 1 : 2); };
+    for (int guard = 0; cframeOn && guard < 4 * kWaveBits; guard++) {
+        Layout fin = lay;
+        if (!storeLayout(fin, false)) return false;
+        int bad = -1;
+        for (int t = 0; t < kWaveBits && bad < 0; t++) {
+            if (!Cnd[t]) continue;
+            const int d = domain(fin.where[t]);
+            bool ok = d >= 0;
+            for (unsigned c = Cnd[t]; c && ok; c &= c - 1) ok = domain(fin.where[__builtin_ctz(c)]) == d;
+            if (!ok) bad = t;
+        }
+        if (bad < 0) break;
+        execConds(nOps, bad);
+    }
+    if (!storeLayout(lay, true)) return false;
+    for (int t = 0; t < kWaveBits; t++) {
+        if (!Cnd[t]) continue;
+        const int w = lay.where[t];
+        for (unsigned c = Cnd[t]; c; c &= c - 1) {
+            const int wc = lay.where[__builtin_ctz(c)];
+            if (inSlot(w))
+                wp.stCondSlot[w] |= 1u << wc;
+            else
+                wp.stCondLane[laneOf(w)] |= 1u << laneOf(wc);
+        }
     }
     for (size_t o = trBeforeStore; o < out.ops.size(); o++) g_waveStoreTrCost += waveTransposeCost(out.ops[o].b);
     // flips still pending: folded into the store offsets

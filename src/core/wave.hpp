@@ -140,6 +140,13 @@ struct WavePass {
     // j ^ stFlip of lane L ^ stFlipLane belongs (stFlipLane: real lane bits
     // 0-5 and the wave bits above them)
     unsigned stFlip = 0, stFlipLane = 0;
+    // conditional flips (deferred CNOTs, planWavePass): the bit of slot s is
+    // further flipped in the registers where the parity of the slots in
+    // stCondSlot[s] is odd; the bit of lane bit l in the lanes where the parity
+    // of the lane bits in stCondLane[l] is odd (real lanes condition real
+    // lanes, wave bits wave bits; vector slots never take part)
+    unsigned stCondSlot[kWaveSlots] = {0};
+    unsigned stCondLane[kWaveLaneBits] = {0};
     int stLane[kWaveLaneBits];
     // The waves of a workgroup run unsynchronised between their loads and
     // stores unless a wave-bit transposition (LDS, two barriers) lies between.
@@ -150,6 +157,22 @@ struct WavePass {
     bool storeBarrier = false;
     bool waveExchange = false;  // the pass has a wave-bit transposition (its barriers order loads before stores)
 };
+
+// Store maps of a pass: register j of lane L (L: real lane bits, then the
+// wave bits) is stored where register waveStReg(wp, j) of lane
+// waveStLane(wp, L) belongs in the store layout (stSlot / stLane / stPos).
+inline int waveStReg(const WavePass& wp, int j) {
+    int r = j ^ (int)wp.stFlip;
+    for (int s = 0; s < kWaveSlots; s++)
+        if (__builtin_popcount((unsigned)j & wp.stCondSlot[s]) & 1) r ^= 1 << s;
+    return r;
+}
+inline int waveStLane(const WavePass& wp, int L) {
+    int r = L ^ (int)wp.stFlipLane;
+    for (int l = 0; l < kWaveLaneBits; l++)
+        if (__builtin_popcount((unsigned)L & wp.stCondLane[l]) & 1) r ^= 1 << l;
+    return r;
+}
 
 // Whether every wave of a tile stores to exactly the addresses it loaded
 // (false: the pass needs storeBarrier or a wave-bit transposition).
@@ -189,6 +212,10 @@ bool waveLowers(const TilePass& ps, const TileOp* ops);
 // pass-balancing cost (PlanHooks::passCost).
 double waveOpCycles(const WaveOp& w);
 double wavePassCycles(const TilePass& ps, const TileOp* ops);
+// The compute-aware planner hooks of wave plans (PlanHooks::passCost /
+// memCost / costMargin): QUEST_PLAN_MEM_CYCLES (0: off) and
+// QUEST_PLAN_COST_MARGIN.
+void waveCostHooks(PlanHooks& hooks);
 // Always-resident low positions for a relabelling wave plan of q.pending:
 // cdefault or cdefault + 1, whichever plans fewer passes (QUEST_WAVE_CMIN_SEARCH
 // =1; default: cdefault); sticky in q.waveCmin until the queue drains.

@@ -249,18 +249,20 @@ void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
         }
     }
     int cnt[32] = {0}, trw = 0, ctl = 0;
+    double cyc = 0;
     for (int i = ps.opBegin; i < ps.opEnd; i++) {
         const WaveOp& w = wp.ops[(size_t)i];
+        cyc += waveOpCycles(w);
         cnt[w.kind]++;
         if (w.kind == (int)WKind::TR && w.b >= kWaveLanes) trw++;
         if (w.kind == (int)WKind::TR) g_trCost += waveTransposeCost(w.b);
         if (w.kind != (int)WKind::DIAG && (w.cReg || w.cLane)) ctl++;
     }
     fprintf(stderr, "wave pass: %d ops  M2 %d M2R %d M2RI %d ANTI %d SWAP %d DIAG %d D2S %d D2L %d TR %d (TRW %d) lane %d "
-            "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d chan %d\n",
+            "ctl %d | ROTY %d ROTX %d HADD %d Y %d phase %d chan %d | cycles %.0f\n",
             ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
             cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
-            cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24]);
+            cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24], cyc);
     int trb[16] = {0};
     for (int i = ps.opBegin; i < ps.opEnd; i++)
         if (wp.ops[(size_t)i].kind == (int)WKind::TR) trb[wp.ops[(size_t)i].b & 15]++;
@@ -287,9 +289,9 @@ void emulateWavePass(real* re, real* im, int L, const WaveProgram& wp, const Wav
     for (int lane = 0; lane < kVLanes; lane++)
         for (int j = 0; j < kWaveRegs; j++) {
             ld[lane][j] = offsetOf(ps.pos, ps.ldSlot, ps.ldLane, lane, j);
-            // relabelling passes store permuted; pending exchanges (stFlip)
-            // store register j where its partner belongs
-            st[lane][j] = offsetOf(ps.stPos, ps.stSlot, ps.stLane, lane ^ (int)ps.stFlipLane, j ^ (int)ps.stFlip);
+            // relabelling passes store permuted; pending exchanges (stFlip,
+            // conditional flips) store register j where its partner belongs
+            st[lane][j] = offsetOf(ps.stPos, ps.stSlot, ps.stLane, waveStLane(ps, lane), waveStReg(ps, j));
         }
     dumpWavePass(wp, ps);
     TilePass tp;

@@ -398,9 +398,6 @@ void flush(QuregImpl& q) { flushImpl(q, false); }
 namespace {
 void flushImpl(QuregImpl& q, bool front) {
     if (q.pending.empty()) return;
-    stats().flushes++;
-    const double tFlush0 = trace::on() ? trace::now() : 0.0;
-    const size_t opsIn = q.pending.size();
     TileProgram prog;
     std::vector<Op> raw;
     if (rt().verify) raw = q.pending;
@@ -413,7 +410,6 @@ void flushImpl(QuregImpl& q, bool front) {
         return e ? atoi(e) : 0;
     }();
     const bool wave = planner == 3 && q.L >= kWaveBits;
-    fuseBlockQubits() = wave ? 1 : 2;
     static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : kWaveVecBits + 5;  // as the HIP backend
     bool channels = false;   // as the HIP backend: density-channel flushes keep one low position fewer
     for (const Op& op : q.pending) channels = channels || op.kind == OpKind::Mat4 || op.kind == OpKind::DensChan2;
@@ -427,6 +423,7 @@ void flushImpl(QuregImpl& q, bool front) {
     hooks.lowPerm = [](const TilePass& ps, const TileOp* ops, int c, int* sigma) {
         return waveLowPerm(ps, ops, c, sigma);
     };
+    waveCostHooks(hooks);
     std::vector<Op> leftover;
     if (front) {
         // as the HIP backend: plain wave queues of wave-sized registers only
@@ -436,6 +433,11 @@ void flushImpl(QuregImpl& q, bool front) {
         hooks.maxPasses = 1;
         hooks.leftover = &leftover;
     }
+    // counted (and global state touched) only once the flush is certain to run
+    stats().flushes++;
+    const double tFlush0 = trace::on() ? trace::now() : 0.0;
+    const size_t opsIn = q.pending.size();
+    fuseBlockQubits() = wave ? 1 : 2;
     std::vector<Op> orig;
     if (relabel && !front) orig = q.pending;
     // as the HIP backend: 6 or 7 always-resident low positions, whichever

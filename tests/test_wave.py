@@ -186,8 +186,9 @@ def test_emulation_orders_waves_like_the_kernel(barrier):
     worst legal order) unless the plan carries the store barrier: planned as
     in round 2 (QUEST_WAVE_NO_STORE_BARRIER=1) it loses unitarity like the
     kernel did; planned with the barrier it is exact."""
-    # QUEST_DIAG_PHASES=0: the round-2 planner's plan of this short queue
-    env = {"QUEST_BACKEND": "cpu", "QUEST_CPU_PLANNER": "3", "QUEST_WAVE_LANE_ORDER": "2", "QUEST_DIAG_PHASES": "0"}
+    # QUEST_DIAG_PHASES=0, QUEST_WAVE_CFRAME=0: the round-2 planner's plan of this short queue
+    env = {"QUEST_BACKEND": "cpu", "QUEST_CPU_PLANNER": "3", "QUEST_WAVE_LANE_ORDER": "2", "QUEST_DIAG_PHASES": "0",
+           "QUEST_WAVE_CFRAME": "0"}
     if not barrier:
         env["QUEST_WAVE_NO_STORE_BARRIER"] = "1"
     out = _run(["-c", RACE], env)
