@@ -108,6 +108,16 @@ void getQuregMemoryPlan(int numQubitsInStateVec, int numRanks, long long out[4])
  * description goes to report. */
 int runCommSelfTest(char* report, int reportLen);
 
+/* Diagnostic: the per-rank footprint of a numQubitsInStateVec-qubit register
+ * on numRanks ranks, shown on THIS single-process job's device next to what it
+ * already holds (e.g. a register of the per-rank size): the exchange buffers of
+ * the plan's largest all-to-all swap are allocated, a one-rank transport
+ * communicator is brought up and the pipelined exchange runs through them.
+ * Returns 1 if the data matched and the buffers are the plan's; the report
+ * gives the plan and the free device memory before / with the buffers / with
+ * the communicator up. */
+int runFootprintCheck(int numQubitsInStateVec, int numRanks, char* report, int reportLen);
+
 /* Restore the canonical qubit layout after distributed qubit remapping. */
 void canonicaliseQureg(Qureg qureg);
 /* physical bit position of each logical qubit of the state-vector */
@@ -130,6 +140,10 @@ typedef struct QuESTStats {
     long long marginalPasses; /* one-pass computations of every qubit's marginal (calcProbOfOutcome cache) */
     long long waveShadowChecks;     /* wave passes compared with the host emulation (tuning "wave_shadow") */
     long long waveShadowMismatches; /* ... that differed from it */
+    long long permutedOps;    /* inner products / addDensityMatrix of registers in different qubit layouts,
+                                 computed by the permuted kernels without a relayout */
+    long long relayouts;      /* canonicalisations that moved data (getAmps, file IO, ... after relabelling) */
+    long long restoreRounds;  /* concurrent rounds of whole-chunk exchanges restoring the chunk placement */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

@@ -82,7 +82,7 @@ class _Binding:
                         ("opsQueued", "passes", "fusedOps", "swaps", "bytesExchanged", "reductions",
                          "verifiedFlushes", "wavePasses", "waveOps", "waveTransposes", "relabels",
                          "globalDiags", "flushes", "marginalPasses", "waveShadowChecks",
-                         "waveShadowMismatches")]
+                         "waveShadowMismatches", "permutedOps", "relayouts", "restoreRounds")]
 
         self.Complex, self.ComplexMatrix2, self.Vector = Complex, ComplexMatrix2, Vector
         self.ComplexArray, self.QASMLogger, self.Qureg = ComplexArray, QASMLogger, Qureg
@@ -143,6 +143,7 @@ class _Binding:
             "setGateFusion": (v, [i]), "getGateFusion": (i, []), "setFusionMaxQubits": (v, [i]),
             "setQuESTTuning": (i, [C.c_char_p, i]), "getQuESTTuning": (i, [C.c_char_p, ip]),
             "getQuregMemoryPlan": (v, [i, i, P(ll)]), "runCommSelfTest": (i, [C.c_char_p, i]),
+            "runFootprintCheck": (i, [i, i, C.c_char_p, i]),
             "flushQureg": (v, [Q]), "syncQureg": (v, [Q]), "copyStateToGPU": (v, [Q]),
             "copyStateFromGPU": (v, [Q]), "copyChunkToBuffers": (v, [Q, C.c_void_p, C.c_void_p]),
             "copyChunkFromBuffers": (v, [Q, C.c_void_p, C.c_void_p]), "canonicaliseQureg": (v, [Q]),
@@ -452,6 +453,13 @@ def runCommSelfTest():
     """(ok, report) of the device transport self-test (quest_amd.h)."""
     buf = C.create_string_buffer(512)
     ok = _call("runCommSelfTest", buf, 512)
+    return bool(ok), buf.value.decode()
+
+
+def runFootprintCheck(num_qubits_in_statevec: int, num_ranks: int):
+    """(ok, report) of the per-rank footprint check (quest_amd.h)."""
+    buf = C.create_string_buffer(1024)
+    ok = _call("runFootprintCheck", int(num_qubits_in_statevec), int(num_ranks), buf, 1024)
     return bool(ok), buf.value.decode()
 
 

@@ -1155,6 +1155,13 @@ int runCommSelfTest(char* report, int reportLen) {
     return ok ? 1 : 0;
 }
 
+int runFootprintCheck(int numQubitsInStateVec, int numRanks, char* report, int reportLen) {
+    std::string r;
+    const bool ok = router::footprintCheck(numQubitsInStateVec, numRanks, r);
+    if (report && reportLen > 0) snprintf(report, (size_t)reportLen, "%s", r.c_str());
+    return ok ? 1 : 0;
+}
+
 void getQuregMemoryPlan(int numQubitsInStateVec, int numRanks, long long out[4]) {
     const router::MemoryPlan m = router::memoryPlan(numQubitsInStateVec, numRanks > 0 ? numRanks : rt().numRanks);
     out[0] = m.state;
@@ -1187,6 +1194,9 @@ void getQuESTStats(QuESTStats* s) {
     s->marginalPasses = stats().marginalPasses;
     s->waveShadowChecks = stats().waveShadowChecks;
     s->waveShadowMismatches = stats().waveShadowMismatches;
+    s->permutedOps = stats().permutedOps;
+    s->relayouts = stats().relayouts;
+    s->restoreRounds = stats().restoreRounds;
 }
 
 void resetQuESTStats(void) { stats() = Stats(); }

@@ -63,8 +63,12 @@ void allgather(const void* send, void* recv, size_t bytesPerRank);
 void barrier();
 std::string describe();
 // Run the device transport's own code paths with a one-rank communicator
-// (HIP build: RCCL); false with a reason if unavailable or wrong.
-bool selfTest(std::string& report);
+// (HIP build: RCCL); false with a reason if unavailable or wrong.  With
+// buffers (nBuf send + nBuf recv comm buffers of bufBytes each, nBuf even):
+// the pipelined exchange runs through them, two sets of nBuf / 2 peers, as
+// a swap with nBuf / 2 peers would use them.
+bool selfTest(std::string& report, void* const* send = nullptr, void* const* recv = nullptr, int nBuf = 0,
+              size_t bufBytes = 0);
 
 }  // namespace comm
 

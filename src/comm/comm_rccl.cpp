@@ -467,8 +467,8 @@ void barrier() {
 // buffering, grouped send + recv -- to itself), the staged scalar allreduce
 // and broadcast, allgather and the async-error watchdog, in one process
 // (several ranks on one GPU: QUEST_RCCL_SHARED_GPU=1 in comm::init).
-bool selfTest(std::string& report) {
-    char msg[512];
+bool selfTest(std::string& report, void* const* userSend, void* const* userRecv, int nBuf, size_t bufBytes) {
+    char msg[768];
     if (g_size != 1 || g_mode != Mode::Single) {
         report = "self-test needs a single-process job";
         return false;
@@ -484,6 +484,46 @@ bool selfTest(std::string& report) {
     g_rank = 0;
     createStreams();
     bool ok = pipelined();
+    size_t freeComm = 0, totalMem = 0;
+    (void)hipMemGetInfo(&freeComm, &totalMem);   // with the communicator up
+    // caller's buffers (a swap's exchange buffers): two sets of nBuf / 2
+    // peers -- every peer is this rank -- through the pipelined exchange,
+    // 4 slices alternating the sets; a byte pattern per buffer and slice,
+    // checked at both ends and in the middle of every receive buffer
+    bool userOk = true;
+    if (userSend && nBuf >= 2) {
+        const int np = nBuf / 2;
+        std::vector<Xfer> xs[2] = {std::vector<Xfer>((size_t)np), std::vector<Xfer>((size_t)np)};
+        const size_t words = bufBytes / 4, probe = std::min<size_t>(words, 1 << 16);
+        std::vector<unsigned> back(probe);
+        auto check = [&](int set, int slice) {
+            for (int p = 0; p < np; p++) {
+                const unsigned want = 0x5a000000u + (unsigned)(slice * 256 + set * np + p);
+                const unsigned* dev = static_cast<const unsigned*>(userRecv[set * np + p]);
+                for (size_t at : {(size_t)0, (words - probe) / 2, words - probe}) {
+                    QA_HIP_CHECK(hipMemcpyAsync(back.data(), dev + at, probe * 4, hipMemcpyDeviceToHost, S()));
+                    hipk::syncStream();
+                    for (size_t i = 0; i < probe; i++) userOk = userOk && back[i] == want;
+                }
+            }
+        };
+        for (int s = 0; s < 4; s++) {
+            const int b = s & 1;
+            for (int p = 0; p < np; p++) {
+                const unsigned pat = 0x5a000000u + (unsigned)(s * 256 + b * np + p);
+                QA_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)userSend[b * np + p], (int)pat, words, S()));
+                xs[b][(size_t)p] = {0, userSend[b * np + p], userRecv[b * np + p], bufBytes};
+            }
+            exchangeAsync(xs[b].data(), np, b);
+            if (s > 0) {
+                exchangeWait(1 - b);
+                check(1 - b, s - 1);
+            }
+        }
+        exchangeWait(1);
+        check(1, 3);
+        ok = ok && userOk;
+    }
     // exchange: 5 slices through 2 buffer sets, as router::multiSwap does
     const size_t N = (size_t)1 << 20;
     std::vector<double> host(N), back(N);
@@ -526,8 +566,12 @@ bool selfTest(std::string& report) {
     watchdog(0.0);
     int v = 0;
     R.getVersion(&v);
-    snprintf(msg, sizeof msg, "RCCL %d (%s): pipelined exchange %s (5 slices, 2 buffer sets), allreduce, broadcast, "
-             "allgather %s", v, g_libName.c_str(), exchangeOk ? "ok" : "WRONG", ok ? "ok" : "WRONG");
+    int at = snprintf(msg, sizeof msg, "RCCL %d (%s): pipelined exchange %s (5 slices, 2 buffer sets), allreduce, "
+                      "broadcast, allgather %s; %.2f GiB free with the communicator up", v, g_libName.c_str(),
+                      exchangeOk ? "ok" : "WRONG", ok ? "ok" : "WRONG", freeComm / 1073741824.0);
+    if (userSend && nBuf >= 2 && at > 0 && at < (int)sizeof msg)
+        snprintf(msg + at, sizeof msg - (size_t)at, "; exchange through the caller's %d x 2 buffers of %.0f MiB %s",
+                 nBuf, bufBytes / 1048576.0, userOk ? "ok" : "WRONG");
     report = msg;
     for (int b = 0; b < 2; b++) {
         QA_HIP_CHECK(hipFree(send[b]));

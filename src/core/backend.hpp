@@ -49,6 +49,11 @@ void writeAmps(QuregImpl& q, i64 local, const real* re, const real* im, i64 n); 
 void readAmps(QuregImpl& q, i64 local, real* re, real* im, i64 n);                // chunk -> host
 void copyState(QuregImpl& dst, QuregImpl& src);
 
+// Move the qubit on every local position p to dest[p] (a permutation of the
+// local positions) by the backend's own means (wave relabelling passes); false
+// if it has none for this register (the caller then uses SWAP ops).
+bool permuteLocal(QuregImpl& q, const int* dest);
+
 // ---- reductions (partials of this chunk) -----------------------------------
 // sum |amp|^2 over amplitudes whose physical bit `bit` == bitVal (bit < 0: all)
 double sumSq(QuregImpl& q, int bit, int bitVal);
@@ -57,6 +62,10 @@ double sumSq(QuregImpl& q, int bit, int bitVal);
 void marginals(QuregImpl& q, double* zeroSums, double* total);
 // sum conj(bra) * ket
 void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]);
+// The same for two registers whose local qubits sit on different positions
+// (no relayout): sig[p] (p < L) = ket's position of the qubit bra holds at
+// local position p; bra's amplitude i pairs with ket's sigma(i).
+void innerProductPerm(QuregImpl& bra, QuregImpl& ket, const int* sig, double out[2]);
 // Density-matrix diagonal: sum over logical row r in [0, 2^n) of Re rho(r,r),
 // restricted to r with logical bit `skipBit` == 0 when skipBit >= 0.  The
 // physical flat index of rho(r,r) is sum_{j : bit j of r} offs[j]; only
@@ -66,6 +75,8 @@ double densDiagSum(QuregImpl& q, const u64* offs, int n, int skipBit, i64 chunkS
 // ---- non-unitary local ops --------------------------------------------------
 // a := alpha a + beta b
 void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta);
+// the same with b's local qubits on other positions (sig as innerProductPerm)
+void axpbyPerm(QuregImpl& a, real alpha, QuregImpl& b, real beta, const int* sig);
 // density matrix from a full pure state held in a comm buffer (2^n amps):
 // element at chunk-local k (global g = chunkStart + k, r = g mod 2^n,
 // c = g div 2^n) := psi_r conj(psi_c)

@@ -286,33 +286,82 @@ void issueRankAnti(QuregImpl& q, const Op& lop) {
     scaleChunk(q, 0, lop.m[b ? 2 : 1]);
 }
 
-// Move the data so that rank r holds logical chunk r again: pairwise
-// whole-chunk exchanges, the same sequence on every rank.
+// Exchange this rank's whole chunk with `peer`'s (every pair of a round calls
+// this at once), pipelined in slices through two buffer sets as in multiSwap:
+// slice s is copied out and exchanged on the communication stream while
+// slice s - 1 is copied in.
+void swapWholeChunk(QuregImpl& q, int peer, i64 slice) {
+    const i64 nSlices = (q.numAmpsPerChunk + slice - 1) / slice;
+    comm::Xfer xs[2];
+    for (i64 s = 0; s < nSlices; s++) {
+        const int b = (int)(s & 1);
+        const i64 off = s * slice, n = std::min(slice, q.numAmpsPerChunk - off);
+        be::toBuffer(q, off, n, g_x.send[(size_t)b], g_x.send[(size_t)b] + n);
+        xs[b] = {peer, g_x.send[(size_t)b], g_x.recv[(size_t)b], sizeof(real) * 2 * (size_t)n};
+        comm::exchangeAsync(&xs[b], 1, b);
+        if (s > 0) {
+            comm::exchangeWait(1 - b);
+            const i64 po = (s - 1) * slice, pn = std::min(slice, q.numAmpsPerChunk - po);
+            be::fromBuffer(q, po, pn, g_x.recv[(size_t)(1 - b)], g_x.recv[(size_t)(1 - b)] + pn);
+        }
+        stats().bytesExchanged += (long long)(sizeof(real) * 2 * n);
+    }
+    const int b = (int)((nSlices - 1) & 1);
+    comm::exchangeWait(b);
+    const i64 po = (nSlices - 1) * slice, pn = std::min(slice, q.numAmpsPerChunk - po);
+    be::fromBuffer(q, po, pn, g_x.recv[(size_t)b], g_x.recv[(size_t)b] + pn);
+}
+
+// Move the data so that rank r holds logical chunk r again.  The chunk at
+// rank r belongs at rank f(r) (its logical id); f is a product of two
+// involutions (per cycle c0 -> c1 -> ... of f: the reflections c_i <-> c_(L-1-i)
+// and then c_j <-> c_(L-j)), so at most two rounds of disjoint pairwise
+// whole-chunk exchanges restore the placement, all pairs of a round at once
+// over their own links.  The X gates on rank qubits that cause such
+// placements make f an involution: one round.  (The round-3 code walked the
+// pairs one after another.)
 void restoreChunks(QuregImpl& q) {
     if (chunksIdentity(q)) return;
     be::flush(q);
-    const i64 slice = std::min<i64>(q.numAmpsPerChunk, std::max<i64>(rt().exchangeSliceBytes / (i64)(2 * sizeof(real)), 1));
-    ensureXBuf(1, slice);
-    const int me = rt().rank;
-    for (int r = 0; r < q.numChunks; r++) {
-        const int s = q.chunkRank[(size_t)r];  // rank holding chunk r
-        if (s == r) continue;
-        int x = 0;  // chunk held by rank r
-        while (q.chunkRank[(size_t)x] != r) x++;
-        if (me == r || me == s) {
-            const int peer = me == r ? s : r;
-            for (i64 off = 0; off < q.numAmpsPerChunk; off += slice) {
-                const i64 n = std::min(slice, q.numAmpsPerChunk - off);
-                be::toBuffer(q, off, n, g_x.send[0], g_x.send[0] + n);
-                comm::sendrecv(peer, g_x.send[0], g_x.recv[0], sizeof(real) * 2 * (size_t)n);
-                be::fromBuffer(q, off, n, g_x.recv[0], g_x.recv[0] + n);
-                stats().bytesExchanged += (long long)(sizeof(real) * 2 * n);
-            }
-            q.chunkId = me == r ? r : x;
+    const int R = q.numChunks, me = rt().rank;
+    std::vector<int> f((size_t)R), rounds[2] = {std::vector<int>((size_t)R), std::vector<int>((size_t)R)};
+    for (int c = 0; c < R; c++) f[(size_t)q.chunkRank[(size_t)c]] = c;
+    for (int r = 0; r < R; r++) rounds[0][(size_t)r] = rounds[1][(size_t)r] = r;
+    std::vector<char> seen((size_t)R, 0);
+    for (int r = 0; r < R; r++) {
+        if (seen[(size_t)r]) continue;
+        std::vector<int> cyc;
+        for (int x = r; !seen[(size_t)x]; x = f[(size_t)x]) {
+            seen[(size_t)x] = 1;
+            cyc.push_back(x);
         }
-        q.chunkRank[(size_t)r] = r;
-        q.chunkRank[(size_t)x] = s;
+        const int L = (int)cyc.size();
+        for (int i = 0; i < L; i++) {
+            rounds[0][(size_t)cyc[(size_t)i]] = cyc[(size_t)(L - 1 - i)];
+            rounds[1][(size_t)cyc[(size_t)i]] = cyc[(size_t)((L - i) % L)];
+        }
     }
+    const i64 slice = std::min<i64>(q.numAmpsPerChunk, std::max<i64>(rt().exchangeSliceBytes / (i64)(2 * sizeof(real)), 1));
+    ensureXBuf(2, slice);
+    for (const std::vector<int>& pairOf : rounds) {
+        bool any = false;
+        for (int r = 0; r < R; r++) any = any || pairOf[(size_t)r] != r;
+        if (!any) continue;
+        stats().restoreRounds++;
+        if (pairOf[(size_t)me] != me) swapWholeChunk(q, pairOf[(size_t)me], slice);
+    }
+    if (trace::on()) {
+        int nr = 0;
+        for (const std::vector<int>& pairOf : rounds)
+            for (int r = 0; r < R; r++)
+                if (pairOf[(size_t)r] != r) {
+                    nr++;
+                    break;
+                }
+        trace::event("restore_chunks", "\"rounds\": %d", nr);
+    }
+    for (int c = 0; c < R; c++) q.chunkRank[(size_t)c] = c;
+    q.chunkId = me;
 }
 
 // Choose the qubits to bring onto local positions for the queued ops (the
@@ -441,7 +490,7 @@ MemoryPlan memoryPlan(int nSV, int numRanks) {
     MemoryPlan m;
     m.state = 2ll * (long long)sizeof(real) << L;
     // multiSwap with k rank qubits: 2 (send, recv) x 2 (double buffer) x
-    // (2^k - 1) peers x slice amps x [re | im]; restoreChunks: one pair
+    // (2^k - 1) peers x slice amps x [re | im]; restoreChunks: one peer
     const i64 partMax = (i64)1 << L;
     for (int k = 1; k <= g; k++) {
         i64 slice = (rt().exchangeSliceBytes >> (k - 1)) / (i64)(2 * sizeof(real));
@@ -449,13 +498,53 @@ MemoryPlan memoryPlan(int nSV, int numRanks) {
         const long long b = 2ll * 2 * ((1ll << k) - 1) * slice * 2 * (long long)sizeof(real);
         m.exchange = std::max(m.exchange, b);
     }
-    if (g > 0) {
+    if (g > 0) {   // restoreChunks: two buffer sets of send + recv
         const i64 slice = std::min<i64>(partMax, std::max<i64>(rt().exchangeSliceBytes / (i64)(2 * sizeof(real)), 1));
-        m.exchange = std::max(m.exchange, 2ll * slice * 2 * (long long)sizeof(real));
+        m.exchange = std::max(m.exchange, 2ll * 2 * slice * 2 * (long long)sizeof(real));
     }
     m.scratch = 64ll << 20;
     m.total = m.state + m.exchange + m.scratch;
     return m;
+}
+
+bool footprintCheck(int nSV, int numRanks, std::string& report) {
+    int g = 0;
+    while ((1 << g) < numRanks) g++;
+    if (g == 0 || (1 << g) != numRanks || rt().numRanks != 1) {
+        report = "footprintCheck: a single-process job and a power-of-two rank count > 1";
+        return false;
+    }
+    const MemoryPlan m = memoryPlan(nSV, numRanks);
+    // the buffers of the largest exchange: a k = g all-to-all (multiSwap)
+    const int L = nSV - g, np = (1 << g) - 1;
+    i64 slice = (rt().exchangeSliceBytes >> (g - 1)) / (i64)(2 * sizeof(real));
+    slice = std::min(std::max<i64>(slice, 16), ((i64)1 << L) >> g);
+    const size_t bytes = sizeof(real) * 2 * (size_t)slice;
+    size_t f0 = 0, f1 = 0, tot = 0;
+    be::deviceSync();
+    const bool known = be::memoryInfo(&f0, &tot);
+    std::vector<void*> send((size_t)(2 * np)), recv((size_t)(2 * np));
+    for (int i = 0; i < 2 * np; i++) {
+        send[(size_t)i] = be::allocComm(bytes);
+        recv[(size_t)i] = be::allocComm(bytes);
+    }
+    be::memoryInfo(&f1, &tot);
+    std::string r;
+    const bool ok = comm::selfTest(r, send.data(), recv.data(), 2 * np, bytes);
+    for (int i = 0; i < 2 * np; i++) {
+        be::freeComm(send[(size_t)i]);
+        be::freeComm(recv[(size_t)i]);
+    }
+    const double G = 1024.0 * 1024 * 1024;
+    char head[512];
+    snprintf(head, sizeof head,
+             "%d qubits on %d ranks: per rank state %.2f GiB + exchange %.3f GiB (%d x 2 buffers of %.0f MiB, the "
+             "k = %d all-to-all) + scratch %.2f GiB = %.2f GiB; device %.2f GiB, free %.2f GiB before the buffers, "
+             "%.2f GiB with them%s; ",
+             nSV, numRanks, m.state / G, 2.0 * 2 * np * bytes / G, 2 * np, bytes / 1048576.0, g, m.scratch / G,
+             m.total / G, tot / G, f0 / G, f1 / G, known ? "" : " (unknown)");
+    report = std::string(head) + r;
+    return ok && (long long)(2 * 2 * np * bytes) == m.exchange;
 }
 
 void create(QuregImpl& q, int nSV, bool density) {
@@ -696,20 +785,48 @@ void densInitPure(QuregImpl& rho, QuregImpl& psi) {
     be::freeComm(fi);
 }
 
+// Two registers of the same shape whose rank qubits and chunk placement agree
+// but whose local qubits may sit on different positions: sig[p] = b's
+// position of the qubit a holds at local position p.  False when their
+// global layouts differ (then both go to the canonical layout).
+static bool localPermutation(const QuregImpl& a, const QuregImpl& b, int* sig) {
+    if (a.L != b.L || a.nSV != b.nSV || a.chunkRank != b.chunkRank || a.chunkId != b.chunkId) return false;
+    for (int j = 0; j < a.nSV; j++) {
+        const int pa = a.l2p[j], pb = b.l2p[j];
+        if ((pa >= a.L || pb >= b.L) && pa != pb) return false;
+        if (pa < a.L) sig[pa] = pb;
+    }
+    return true;
+}
+
+// QUEST_PERM_KERNELS=0: relayout both registers as before round 4
+static bool permKernels() {
+    static const bool on = !getenv("QUEST_PERM_KERNELS") || atoi(getenv("QUEST_PERM_KERNELS")) != 0;
+    return on;
+}
+
 void axpby(QuregImpl& a, real alpha, QuregImpl& b, real beta) {
     drain(a);  // routing may move qubits: compare layouts afterwards
     drain(b);
-    if (memcmp(a.l2p, b.l2p, sizeof(int) * a.nSV) != 0 || a.chunkRank != b.chunkRank) {
+    int sig[64];
+    if (memcmp(a.l2p, b.l2p, sizeof(int) * a.nSV) == 0 && a.chunkRank == b.chunkRank) {
+        be::axpby(a, alpha, b, beta);
+    } else if (permKernels() && localPermutation(a, b, sig)) {
+        // b read in a's layout by the permuted kernel: no relayout of either
+        stats().permutedOps++;
+        be::axpbyPerm(a, alpha, b, beta, sig);
+    } else {
         canonicalise(a);
         canonicalise(b);
+        be::axpby(a, alpha, b, beta);
     }
-    be::axpby(a, alpha, b, beta);
     a.stateGen++;
 }
 
 void canonicalise(QuregImpl& q) {
     drain(q);
     if (q.permIdentity() && chunksIdentity(q)) return;
+    stats().relayouts++;
     // 1. the right logical qubit on every global position, in all-to-all
     //    rounds: first every global position whose qubit is local comes in;
     //    qubits stuck on the wrong global position are first moved out to
@@ -741,7 +858,21 @@ void canonicalise(QuregImpl& q) {
     }
     // 2. every rank holds its own chunk again (undo X-gate relabellings)
     restoreChunks(q);
-    // 3. permute local qubits with local SWAP ops
+    // 3. permute local qubits: op-free relabelling passes of the wave engine
+    //    (a permuted store, up to 12 qubits per HBM round trip), else SWAP ops
+    {
+        int dest[64];
+        bool moved = false;
+        for (int p = 0; p < q.L; p++) {
+            dest[p] = q.p2l[p];
+            moved = moved || dest[p] != p;
+        }
+        static const bool relayout = !getenv("QUEST_RELAYOUT_PASSES") || atoi(getenv("QUEST_RELAYOUT_PASSES")) != 0;
+        if (moved && relayout && be::permuteLocal(q, dest)) {
+            for (int p = 0; p < q.L; p++) q.l2p[p] = q.p2l[p] = p;
+            return;
+        }
+    }
     static const cplx kSwap[16] = {{1, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 0}, {0, 0},
                                    {0, 0}, {1, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 0}};
     for (int i = 0; i < q.L; i++) {
@@ -856,13 +987,21 @@ double densTrace(QuregImpl& q) { return densDiag(q, -1); }
 cplx inner(QuregImpl& bra, QuregImpl& ket) {
     drain(bra);  // routing may move qubits: compare layouts afterwards
     drain(ket);
-    if (memcmp(bra.l2p, ket.l2p, sizeof(int) * bra.nSV) != 0 || bra.chunkRank != ket.chunkRank) {
-        canonicalise(bra);
-        canonicalise(ket);
-    }
     stats().reductions++;
     double v[2];
-    be::innerProduct(bra, ket, v);
+    int sig[64];
+    if (memcmp(bra.l2p, ket.l2p, sizeof(int) * bra.nSV) == 0 && bra.chunkRank == ket.chunkRank) {
+        be::innerProduct(bra, ket, v);
+    } else if (permKernels() && localPermutation(bra, ket, sig)) {
+        // the reference sums locally and allreduces (QuEST_cpu_distributed.c:41-51);
+        // so does this, with ket read in bra's layout -- no relayout
+        stats().permutedOps++;
+        be::innerProductPerm(bra, ket, sig, v);
+    } else {
+        canonicalise(bra);
+        canonicalise(ket);
+        be::innerProduct(bra, ket, v);
+    }
     if (comm::active()) comm::allreduceSum(v, 2);
     return {(real)v[0], (real)v[1]};
 }

@@ -15,6 +15,8 @@
 //  * reductions are chunk partials + one allreduce.
 #pragma once
 
+#include <string>
+
 #include "core.hpp"
 
 namespace qa {
@@ -28,6 +30,13 @@ struct MemoryPlan {
     long long state = 0, exchange = 0, scratch = 0, total = 0;
 };
 MemoryPlan memoryPlan(int nSV, int numRanks);
+// The per-rank footprint of an nSV-qubit register on numRanks ranks, on this
+// (single-process) job's device next to whatever it already holds: the
+// exchange buffers of the plan's largest all-to-all swap allocated as
+// multiSwap would, a transport communicator brought up and the pipelined
+// exchange run through them (comm::selfTest).  Free device memory before,
+// with the buffers and with the communicator up goes to report.
+bool footprintCheck(int nSV, int numRanks, std::string& report);
 
 void create(QuregImpl& q, int nSV, bool density);
 void destroy(QuregImpl& q);
@@ -89,6 +98,9 @@ struct Stats {
     long long flushes = 0;        // backend queue flushes (each planned into passes)
     long long marginalPasses = 0; // one-pass all-qubit marginals (probZero cache fills)
     long long waveShadowChecks = 0, waveShadowMismatches = 0;  // rt().waveShadow
+    long long permutedOps = 0;    // inner products / axpby of registers in different layouts, no relayout
+    long long relayouts = 0;      // canonicalisations that moved data
+    long long restoreRounds = 0;  // concurrent rounds of whole-chunk exchanges restoring chunk placement
 };
 Stats& stats();
 

@@ -209,13 +209,13 @@ bool waveLowPerm(const TilePass& ps, const TileOp* ops, int cmin, int* sigma) {
                                                           : !(kWaveSlots == 5 && kWaveWBits == 2);
     for (int p = 0; p < 64; p++) sigma[p] = p;
     if (!on || ps.k != kWaveBits) return false;
-    const Stats keep = stats();
-    const long long keepTr = g_waveStoreTrCost;
     WaveProgram tmp;
     int endLanes[3];
-    const bool ok = planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp, endLanes);
-    stats() = keep;
-    g_waveStoreTrCost = keepTr;
+    bool ok;
+    {
+        QuietPlan quiet;
+        ok = planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp, endLanes);
+    }
     if (!ok) return false;
     constexpr int VB = kWaveVecBits;
     // tile bits stored to the always-resident positions [VB, cmin)
@@ -265,7 +265,7 @@ int& waveLaneOrder() {
 }
 
 bool relabelsLower(const TileProgram& prog) {
-    const Stats keep = stats();
+    QuietPlan quiet;
     bool ok = true;
     for (const TilePass& ps : prog.passes) {
         bool perm = false;
@@ -277,20 +277,16 @@ bool relabelsLower(const TileProgram& prog) {
             break;
         }
     }
-    stats() = keep;
     return ok;
 }
 
 long long g_waveStoreTrCost = 0;
+thread_local int t_planQuiet = 0;
 
 bool waveLowers(const TilePass& ps, const TileOp* ops) {
-    const Stats keep = stats();
-    const long long keepTr = g_waveStoreTrCost;
+    QuietPlan quiet;
     WaveProgram tmp;
-    const bool ok = planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp);
-    stats() = keep;
-    g_waveStoreTrCost = keepTr;
-    return ok;
+    return planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp);
 }
 
 // Issue cycles per wave of one op (uncontrolled), from the measured cost of
@@ -331,16 +327,13 @@ double waveOpCycles(const WaveOp& w) {
 }
 
 double wavePassCycles(const TilePass& ps, const TileOp* ops) {
-    const Stats keep = stats();
-    const long long keepTr = g_waveStoreTrCost;
+    QuietPlan quiet;
     WaveProgram tmp;
     double c = -1;
     if (planWavePass(ps, ops, ps.opEnd - ps.opBegin, tmp)) {
         c = 0;
         for (const WaveOp& w : tmp.ops) c += waveOpCycles(w);
     }
-    stats() = keep;
-    g_waveStoreTrCost = keepTr;
     return c;
 }
 
@@ -373,8 +366,7 @@ int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks) {
     PlanHooks trialHooks;
     trialHooks.relabelOk = hooks.relabelOk;
     trialHooks.lowPerm = hooks.lowPerm;
-    const Stats keep = stats();
-    const long long keepTr = g_waveStoreTrCost;
+    QuietPlan quiet;
     size_t best = (size_t)-1;
     int choice = cdefault;
     for (int c = cdefault; c <= cdefault + 1 && c < kWaveBits - 1; c++) {
@@ -386,8 +378,6 @@ int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks) {
             choice = c;
         }
     }
-    stats() = keep;
-    g_waveStoreTrCost = keepTr;
     q.waveCmin = choice;
     return choice;
 }
@@ -400,6 +390,112 @@ void applyProgramPerm(QuregImpl& q, const TileProgram& prog) {
     for (int lg = 0; lg < q.nSV; lg++)
         if (q.l2p[lg] < q.L) q.l2p[lg] = prog.perm[q.l2p[lg]];
     for (int lg = 0; lg < q.nSV; lg++) q.p2l[q.l2p[lg]] = lg;
+}
+
+bool planRelayout(int L, const int* destIn, TileProgram& prog) {
+    constexpr int VB = kWaveVecBits, K = kWaveBits, fixedLow = kWaveVecBits + 3;
+    prog.passes.clear();
+    prog.ops.clear();
+    prog.phases.clear();
+    prog.perm.resize((size_t)L);
+    for (int x = 0; x < L; x++) prog.perm[(size_t)x] = x;
+    if (L < K) return false;
+    int dest[64];
+    for (int p = 0; p < L; p++) dest[p] = destIn[p];
+    for (int v = 0; v < VB; v++)
+        if (dest[v] != v) return false;   // the vector bits never move in a wave pass
+    for (int guard = 0; guard < 4 * L; guard++) {
+        bool done = true;
+        for (int p = 0; p < L && done; p++) done = dest[p] == p;
+        if (done) return true;
+        // the tile: positions 0 .. fixedLow-1 (every wave tile holds them),
+        // then whole cycles of dest that fit (those through the fixed low
+        // positions first), then a run of the next cycle
+        std::vector<char> inT((size_t)L, 0);
+        int count = 0;
+        for (int p = 0; p < fixedLow; p++) inT[(size_t)p] = 1, count++;
+        std::vector<std::vector<int>> cycles;
+        std::vector<char> seen((size_t)L, 0);
+        for (int p = 0; p < L; p++) {
+            if (seen[(size_t)p] || dest[p] == p) continue;
+            std::vector<int> c;
+            for (int x = p; !seen[(size_t)x]; x = dest[x]) {
+                seen[(size_t)x] = 1;
+                c.push_back(x);
+            }
+            cycles.push_back(c);
+        }
+        auto touchesLow = [&](const std::vector<int>& c) {
+            for (int x : c)
+                if (x < fixedLow) return true;
+            return false;
+        };
+        std::stable_sort(cycles.begin(), cycles.end(), [&](const std::vector<int>& a, const std::vector<int>& b) {
+            const bool la = touchesLow(a), lb = touchesLow(b);
+            if (la != lb) return la;
+            return a.size() < b.size();
+        });
+        for (const std::vector<int>& c : cycles) {
+            int missing = 0;
+            for (int x : c) missing += !inT[(size_t)x];
+            if (count + missing <= K) {
+                for (int x : c)
+                    if (!inT[(size_t)x]) inT[(size_t)x] = 1, count++;
+                continue;
+            }
+            if (count >= K) break;
+            // a run c_a, c_a+1, ... from a member already in the tile (else c_0)
+            const int m = (int)c.size();
+            int a = 0;
+            for (int i = 0; i < m; i++)
+                if (inT[(size_t)c[(size_t)i]]) {
+                    a = i;
+                    break;
+                }
+            for (int i = 0; i < m && count < K; i++) {
+                const int x = c[(size_t)((a + i) % m)];
+                if (!inT[(size_t)x]) inT[(size_t)x] = 1, count++;
+            }
+        }
+        for (int p = 0; p < L && count < K; p++)
+            if (!inT[(size_t)p]) inT[(size_t)p] = 1, count++;
+        // within the tile: every qubit whose destination is in the tile goes
+        // there; the others take the positions nobody in the tile moves to
+        int pi[64];
+        std::vector<char> taken((size_t)L, 0);
+        std::vector<int> waiting;
+        for (int p = 0; p < L; p++) {
+            if (!inT[(size_t)p]) continue;
+            if (inT[(size_t)dest[p]]) {
+                pi[p] = dest[p];
+                taken[(size_t)dest[p]] = 1;
+            } else {
+                waiting.push_back(p);
+            }
+        }
+        size_t w = 0;
+        for (int p = 0; p < L; p++)
+            if (inT[(size_t)p] && !taken[(size_t)p]) pi[waiting[w++]] = p;
+        TilePass ps;
+        ps.k = K;
+        int n = 0;
+        for (int p = 0; p < L; p++)
+            if (inT[(size_t)p]) {
+                ps.pos[n] = p;
+                ps.stPos[n++] = pi[p];
+                ps.qmask |= 1ull << p;
+            }
+        ps.opBegin = ps.opEnd = (int)prog.ops.size();
+        if (!waveLowers(ps, prog.ops.data())) return false;
+        prog.passes.push_back(ps);
+        int nd[64];
+        for (int p = 0; p < L; p++) nd[p] = dest[p];
+        for (int p = 0; p < L; p++)
+            if (inT[(size_t)p]) nd[pi[p]] = dest[p];
+        for (int p = 0; p < L; p++) dest[p] = nd[p];
+        for (int x = 0; x < L; x++) prog.perm[(size_t)x] = inT[(size_t)prog.perm[(size_t)x]] ? pi[prog.perm[(size_t)x]] : prog.perm[(size_t)x];
+    }
+    return false;
 }
 
 int waveTransposeCost(int laneBit) { return laneBit >= kWaveLanes ? 3 : laneBit >= 4 ? 1 : laneBit >= 2 ? 2 : 4; }
@@ -1198,7 +1294,8 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 wp.stCondLane[laneOf(w)] |= 1u << laneOf(wc);
         }
     }
-    for (size_t o = trBeforeStore; o < out.ops.size(); o++) g_waveStoreTrCost += waveTransposeCost(out.ops[o].b);
+    if (!t_planQuiet)
+        for (size_t o = trBeforeStore; o < out.ops.size(); o++) g_waveStoreTrCost += waveTransposeCost(out.ops[o].b);
     // flips still pending: folded into the store offsets
     wp.stFlip = slotFlips();
     wp.stFlipLane = laneFlips();
@@ -1212,6 +1309,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     static const bool noBarrier = getenv("QUEST_WAVE_NO_STORE_BARRIER") && atoi(getenv("QUEST_WAVE_NO_STORE_BARRIER"));
     wp.storeBarrier = !wp.waveExchange && !waveStoresInPlace(wp) && !noBarrier;
     out.passes.push_back(wp);
+    if (t_planQuiet) return true;   // a trial plan: the statistics are the launched passes'
     stats().waveOps += wp.opEnd - wp.opBegin;
     for (int o = wp.opBegin; o < wp.opEnd; o++) stats().waveTransposes += out.ops[o].kind == (int)WKind::TR;
     return true;

@@ -222,11 +222,27 @@ void waveCostHooks(PlanHooks& hooks);
 int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks);
 // After a program ran: the register's qubits moved by prog.perm.
 void applyProgramPerm(QuregImpl& q, const TileProgram& prog);
+// A local qubit permutation as op-free relabelling wave passes (load a tile,
+// store it with its positions permuted: no arithmetic, one HBM round trip per
+// pass, at most 12 moved positions each): dest[p] = the position the qubit on
+// local position p must move to.  False if the wave engine cannot (a moved
+// vector bit, or a pass it does not lower); prog.passes then is unusable.
+bool planRelayout(int L, const int* dest, TileProgram& prog);
 
 // Cost in VALU instructions per lane of one transposition with lane bit l
 // (for the planner's statistics and tests).
 int waveTransposeCost(int laneBit);
 extern long long g_waveStoreTrCost;   // planner study: weighted transpositions for the store layout
+// Plans made while a QuietPlan lives on this thread (lowering checks, cost
+// estimates, trial plans -- possibly on planner worker threads) leave the
+// global statistics alone.
+extern thread_local int t_planQuiet;
+struct QuietPlan {
+    QuietPlan() { t_planQuiet++; }
+    ~QuietPlan() { t_planQuiet--; }
+    QuietPlan(const QuietPlan&) = delete;
+    QuietPlan& operator=(const QuietPlan&) = delete;
+};
 
 // Load layout of the bits beyond the slots (QUEST_WAVE_LANE_ORDER / tuning
 // "wave_lane_order"): 1 (default) lanes 3-5 take the lowest positions, 0 need

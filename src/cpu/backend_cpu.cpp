@@ -612,6 +612,62 @@ void innerProduct(QuregImpl& bra, QuregImpl& ket, double out[2]) {
     out[1] = i;
 }
 
+namespace {
+// sigma(i) of the permuted kernels: the bits of i moved to sig[] positions,
+// through two 2^h tables
+struct BitMap {
+    int h;
+    std::vector<i64> lo, hi;
+    BitMap(int L, const int* sig) : h(L / 2), lo((size_t)1 << (L / 2)), hi((size_t)1 << (L - L / 2)) {
+        for (size_t x = 0; x < lo.size(); x++)
+            for (int b = 0; b < h; b++)
+                if ((x >> b) & 1) lo[x] |= (i64)1 << sig[b];
+        for (size_t x = 0; x < hi.size(); x++)
+            for (int b = 0; b < L - h; b++)
+                if ((x >> b) & 1) hi[x] |= (i64)1 << sig[h + b];
+    }
+    i64 operator()(i64 i) const { return lo[(size_t)(i & (((i64)1 << h) - 1))] | hi[(size_t)(i >> h)]; }
+};
+}  // namespace
+
+bool permuteLocal(QuregImpl& q, const int* dest) {
+    // the wave engine's relayout passes on its host emulation (QUEST_CPU_PLANNER=3)
+    static const bool wave = getenv("QUEST_CPU_PLANNER") && atoi(getenv("QUEST_CPU_PLANNER")) == 3;
+    if (!wave || q.L < kWaveBits + 6 || rt().verify) return false;
+    TileProgram prog;
+    if (!planRelayout(q.L, dest, prog)) return false;
+    flush(q);
+    runProgram(q.re, q.im, q.L, prog, true);
+    return true;
+}
+
+void innerProductPerm(QuregImpl& bra, QuregImpl& ket, const int* sig, double out[2]) {
+    flush(bra);
+    flush(ket);
+    const BitMap map(bra.L, sig);
+    double r = 0, i = 0;
+#pragma omp parallel for reduction(+ : r, i) if (bra.numAmpsPerChunk >= kOmpMin)
+    for (i64 k = 0; k < bra.numAmpsPerChunk; k++) {
+        const i64 j = map(k);
+        r += (double)bra.re[k] * ket.re[j] + (double)bra.im[k] * ket.im[j];
+        i += (double)bra.re[k] * ket.im[j] - (double)bra.im[k] * ket.re[j];
+    }
+    out[0] = r;
+    out[1] = i;
+}
+
+void axpbyPerm(QuregImpl& a, real alpha, QuregImpl& b, real beta, const int* sig) {
+    flush(a);
+    flush(b);
+    const BitMap map(a.L, sig);
+#pragma omp parallel for if (a.numAmpsPerChunk >= kOmpMin)
+    for (i64 k = 0; k < a.numAmpsPerChunk; k++) {
+        const i64 j = map(k);
+        a.re[k] = alpha * a.re[k] + beta * b.re[j];
+        a.im[k] = alpha * a.im[k] + beta * b.im[j];
+    }
+}
+
 double densDiagSum(QuregImpl& q, const u64* offs, int n, int skipBit, i64 chunkStart) {
     flush(q);
     double s = 0;

@@ -2,6 +2,7 @@
 // All grid-stride, 256 threads, 16-byte vector accesses where the layout
 // allows; launched on the backend stream.
 #include <algorithm>
+#include <cstring>
 
 #include "qa_hip.h"
 
@@ -286,9 +287,88 @@ void launchCopyVec(void* dst, const void* src, size_t bytes, hipStream_t st) {
     QA_HIP_CHECK(hipGetLastError());
 }
 
+// a = alpha a + beta b, b in another qubit layout (PermArgs): per tile, b's
+// runs into LDS in a's element order, then a streamed in place
+template <typename T>
+__global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, T* __restrict__ ai, T alpha,
+                                                            const T* __restrict__ br, const T* __restrict__ bi,
+                                                            T beta, PermArgs pa) {
+    extern __shared__ unsigned char smem[];
+    T* sr = reinterpret_cast<T*>(smem);
+    T* si = sr + (1 << pa.K);
+    const int E = 1 << pa.K;
+    const long long tiles = 1ll << pa.nOut;
+    for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
+        const unsigned long long baseB = scatterBits((unsigned long long)t, pa.oB, pa.nOut);
+        for (int f = threadIdx.x; f < E; f += kThreads) {
+            unsigned long long ob = 0;
+            int e = 0;
+            for (int m = 0; m < pa.K; m++)
+                if ((f >> m) & 1) {
+                    ob |= 1ull << pa.tB[pa.bOrd[m]];
+                    e |= 1 << pa.bOrd[m];
+                }
+            sr[e] = br[baseB | ob];
+            si[e] = bi[baseB | ob];
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < E; e += kThreads) {
+            const unsigned long long oa = baseA | scatterBits((unsigned long long)e, pa.tA, pa.K);
+            ar[oa] = alpha * ar[oa] + beta * sr[e];
+            ai[oa] = alpha * ai[oa] + beta * si[e];
+        }
+        __syncthreads();
+    }
+}
+
+
 void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n) {
     hipLaunchKernelGGL(axpbyKernel<real>, dim3(gridFor(n / Vec16<real>::n)), dim3(kThreads), 0, stream(), ar, ai,
                        alpha, br, bi, beta, n);
+    QA_HIP_CHECK(hipGetLastError());
+}
+
+PermArgs makePermArgs(int L, const int* sig) {
+    PermArgs pa;
+    std::memset(&pa, 0, sizeof pa);
+    // tile: a's positions 0-3, those b holds on 0-3, then the lowest others
+    bool inTile[64] = {false};
+    int inv[64];
+    for (int p = 0; p < L; p++) inv[sig[p]] = p;
+    const int c = std::min(L, 4);
+    for (int p = 0; p < c; p++) inTile[p] = inTile[inv[p]] = true;
+    const int K = std::min(L, 10);
+    int k = 0;
+    for (int p = 0; p < L; p++) k += inTile[p];
+    for (int p = 0; p < L && k < K; p++)
+        if (!inTile[p]) inTile[p] = true, k++;
+    pa.K = k;
+    int n = 0, m = 0;
+    for (int p = 0; p < L; p++) {
+        if (inTile[p]) {
+            pa.tA[n] = (signed char)p;
+            pa.tB[n++] = (signed char)sig[p];
+        } else {
+            pa.oA[m] = (signed char)p;
+            pa.oB[m++] = (signed char)sig[p];
+        }
+    }
+    pa.nOut = m;
+    // b order: tile bits by ascending b-position
+    int ord[16];
+    for (int x = 0; x < n; x++) ord[x] = x;
+    std::sort(ord, ord + n, [&](int a, int b) { return pa.tB[a] < pa.tB[b]; });
+    for (int x = 0; x < n; x++) pa.bOrd[x] = (signed char)ord[x];
+    return pa;
+}
+
+void launchAxpbyPerm(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, const PermArgs& pa) {
+    const long long tiles = 1ll << pa.nOut;
+    const int grid = (int)std::min<long long>(tiles, 8ll * numCUs());
+    const size_t lds = 2 * sizeof(real) << pa.K;
+    hipLaunchKernelGGL(axpbyPermKernel<real>, dim3(grid), dim3(kThreads), lds, stream(), ar, ai, alpha, br, bi, beta,
+                       pa);
     QA_HIP_CHECK(hipGetLastError());
 }
 

@@ -11,6 +11,8 @@
 // after copying the whole state back (:1121, :1143-1163).
 #include "qa_hip.h"
 
+#include <algorithm>
+
 namespace qa {
 namespace hipk {
 
@@ -256,6 +258,49 @@ __global__ __launch_bounds__(kThreads) void innerKernel(const T* __restrict__ ar
     }
 }
 
+// sum conj(a_i) b_sigma(i) with b in another qubit layout (PermArgs): per
+// tile, b's 16-element runs into LDS in a's element order, then a streamed
+template <typename T>
+__global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict__ ar, const T* __restrict__ ai,
+                                                            const T* __restrict__ br, const T* __restrict__ bi,
+                                                            PermArgs pa, double* __restrict__ part) {
+    extern __shared__ unsigned char smem[];
+    T* sr = reinterpret_cast<T*>(smem);
+    T* si = sr + (1 << pa.K);
+    const int E = 1 << pa.K;
+    const long long tiles = 1ll << pa.nOut;
+    double accR = 0, accI = 0;
+    for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
+        const unsigned long long baseB = scatterBits((unsigned long long)t, pa.oB, pa.nOut);
+        for (int f = threadIdx.x; f < E; f += kThreads) {
+            unsigned long long ob = 0;
+            int e = 0;
+            for (int m = 0; m < pa.K; m++)
+                if ((f >> m) & 1) {
+                    ob |= 1ull << pa.tB[pa.bOrd[m]];
+                    e |= 1 << pa.bOrd[m];
+                }
+            sr[e] = br[baseB | ob];
+            si[e] = bi[baseB | ob];
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < E; e += kThreads) {
+            const unsigned long long oa = baseA | scatterBits((unsigned long long)e, pa.tA, pa.K);
+            const double x = ar[oa], y = ai[oa], u = sr[e], v = si[e];
+            accR += x * u + y * v;
+            accI += x * v - y * u;
+        }
+        __syncthreads();
+    }
+    const double s0 = blockSum(accR);
+    const double s1 = blockSum(accI);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = s0;
+        part[kMaxBlocks + blockIdx.x] = s1;
+    }
+}
+
 struct Offs {
     unsigned long long o[32];
 };
@@ -432,6 +477,18 @@ void reduceInner(const real* ar, const real* ai, const real* br, const real* bi,
     ensureScratch();
     const int nb = blocksFor(n / Vec16<real>::n);
     hipLaunchKernelGGL(innerKernel<real>, dim3(nb), dim3(kThreads), 0, stream(), ar, ai, br, bi, n, g_partials);
+    QA_HIP_CHECK(hipGetLastError());
+    finish(nb, 2, out);
+}
+
+void reduceInnerPerm(const real* ar, const real* ai, const real* br, const real* bi, const PermArgs& pa,
+                     double out[2]) {
+    ensureScratch();
+    const long long tiles = 1ll << pa.nOut;
+    const int nb = (int)std::min<long long>(tiles, kMaxBlocks);
+    const size_t lds = 2 * sizeof(real) << pa.K;
+    hipLaunchKernelGGL(innerPermKernel<real>, dim3(nb), dim3(kThreads), lds, stream(), ar, ai, br, bi, pa,
+                       g_partials);
     QA_HIP_CHECK(hipGetLastError());
     finish(nb, 2, out);
 }

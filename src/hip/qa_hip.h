@@ -106,6 +106,14 @@ __device__ __forceinline__ void streamStore(V* p, V v) {
     }
 }
 
+// PermArgs helpers: the bits of x scattered to positions pos[0..n)
+__device__ __forceinline__ unsigned long long scatterBits(unsigned long long x, const signed char* pos, int n) {
+    unsigned long long r = 0;
+    for (int m = 0; m < n; m++)
+        if ((x >> m) & 1) r |= 1ull << pos[m];
+    return r;
+}
+
 #endif  // __HIPCC__
 
 // Tile size of the compile-time tile kernel (2^K amplitudes, 256 threads x
@@ -125,6 +133,21 @@ struct TileArgs {
     int pos[32];         // tile bit -> physical bit
 };
 
+// Two registers of one rank whose local qubits sit on different positions:
+// amplitude i of `a` pairs with amplitude sigma(i) of `b`, sigma a permutation
+// of the index bits (a's position p -> b's position sig[p]).  The permuted
+// kernels (innerPermKernel, axpbyPermKernel) take tiles of 2^K amplitudes
+// whose a-positions include 0-3 and every position b holds on 0-3, so both
+// sides load 16-element runs; b goes through LDS into a's order.
+struct PermArgs {
+    int K;                    // tile bits
+    int nOut;                 // the other bits (L - K)
+    signed char tA[16], tB[16];  // tile bit k: position in a / in b
+    signed char bOrd[16];     // b-order bit m (b-positions ascending) -> tile bit k
+    signed char oA[48], oB[48];  // other bit m: position in a / in b
+};
+PermArgs makePermArgs(int L, const int* sig);
+
 // ---- launchers (defined in kernels_*.hip) ----------------------------------
 void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps, const TilePhase* dPhases,
                     const real* dMats, int mode);
@@ -141,6 +164,8 @@ void launchCopyVec(void* dst, const void* src, size_t bytes, hipStream_t st);
 void launchPackBits(const real* re, const real* im, const int* pos, int k, u64 setMask, i64 start, i64 count,
                     real* br, real* bi, bool unpack);
 void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n);
+// a = alpha a + beta b with b's amplitude sigma(i) for a's i (PermArgs)
+void launchAxpbyPerm(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, const PermArgs& pa);
 void launchDensInitPure(real* re, real* im, i64 n, const real* pr, const real* pi, int nq, i64 chunkStart);
 
 // reductions: results are written to `out` (device, doubles) and copied back
@@ -148,6 +173,9 @@ double reduceSumSq(const real* re, const real* im, i64 n, int bit, int bitVal);
 // zeroSums[b] = sum |a_i|^2 over i with bit b clear (b < L), *total = sum |a_i|^2, one pass
 void reduceMarginals(const real* re, const real* im, int L, double* zeroSums, double* total);
 void reduceInner(const real* ar, const real* ai, const real* br, const real* bi, i64 n, double out[2]);
+// sum conj(a_i) b_sigma(i) (PermArgs: one streaming pass over both, no relayout)
+void reduceInnerPerm(const real* ar, const real* ai, const real* br, const real* bi, const PermArgs& pa,
+                     double out[2]);
 double reduceMaxDiff(const real* ar, const real* ai, const real* br, const real* bi, i64 n);
 double reduceDensDiag(const real* re, i64 chunkAmps, const u64* offs, int nq, int skipBit, i64 chunkStart);
 double reduceDensFidelity(const real* re, const real* im, i64 n, const real* pr, const real* pi, int nq,

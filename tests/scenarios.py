@@ -267,3 +267,40 @@ def hang_rank1(env):
 
 
 SCENARIOS["hang_rank1"] = hang_rank1
+
+
+def restore_chunks(env):
+    """X on every rank qubit relabels chunks (chunk c held by rank c ^ 7 on 8
+    ranks); a read then restores the placement.  That permutation is an
+    involution: ONE concurrent round of pairwise whole-chunk exchanges, one
+    chunk per rank.  CNOTs among rank qubits make longer cycles: at most two
+    rounds (a permutation is a product of two involutions)."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    n = 9
+    r = qa.Register(env, n)
+    r.init_plus()
+    random_layered(n, 2, seed=8).apply(r)
+    capi.canonicaliseQureg(r.q)
+    capi.resetQuESTStats()
+    for q in (8, 7, 6):
+        r.x(q)
+    out = {"xor": r.to_numpy()}
+    st = capi.getQuESTStats()
+    out["_xor_rounds"], out["_xor_bytes"] = st["restoreRounds"], st["bytesExchanged"]
+    capi.resetQuESTStats()
+    r.x(8)
+    r.cnot(8, 7)
+    r.x(6)
+    r.cnot(7, 6)
+    r.cnot(6, 8)
+    out["cycles"] = r.to_numpy()
+    st = capi.getQuESTStats()
+    out["_cyc_rounds"], out["_cyc_swaps"] = st["restoreRounds"], st["swaps"]
+    r.close()
+    return out
+
+
+SCENARIOS["restore_chunks"] = restore_chunks

@@ -105,6 +105,23 @@ def test_eight_ranks(env, tmp_path, name):
             np.testing.assert_allclose(np.asarray(g), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
 
 
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_restore_chunks_in_concurrent_rounds(env, tmp_path, ranks):
+    """Chunk placement restored by concurrent rounds of pairwise whole-chunk
+    exchanges (router restoreChunks): X on the rank qubits is one round that
+    moves exactly one chunk per rank; CNOTs among rank qubits at most two."""
+    want = _single("restore_chunks", env)
+    got = _multi("restore_chunks", ranks, tmp_path)
+    for k, v in want.items():
+        if k.startswith("_"):
+            continue
+        np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+    chunk_bytes = 16 * (1 << (9 - {2: 1, 8: 3}[ranks]))
+    assert int(got["_xor_rounds"]) == 1
+    assert int(got["_xor_bytes"]) == chunk_bytes
+    assert 1 <= int(got["_cyc_rounds"]) <= 2
+
+
 def test_bench_under_torchrun_host_build():
     """bench.py in the driver's launch shape (torch.distributed.run, 4 ranks,
     127.0.0.1 rendezvous) on the host build: one JSON line from rank 0 with
