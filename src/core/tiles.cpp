@@ -647,7 +647,8 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         int frontEnd = first;
         for (int c = 0; frontEnd < n && c < frontN; frontEnd++)
             if (!done[frontEnd]) c++;
-        static const double beta = getenv("QUEST_PLAN_LOOKAHEAD") ? atof(getenv("QUEST_PLAN_LOOKAHEAD")) : 0.0;
+        static const double betaEnv = getenv("QUEST_PLAN_LOOKAHEAD") ? atof(getenv("QUEST_PLAN_LOOKAHEAD")) : 0.0;
+        const double beta = hooks && hooks->lookahead >= 0 ? hooks->lookahead : betaEnv;
         std::vector<int> nextTake;
         auto score = [&](const std::vector<int>& v) {
             int f = 0;
@@ -666,10 +667,11 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             return sc;
         };
         double bestScore = score(best);
-        static const int maxSeeds = [] {
+        static const int maxSeedsEnv = [] {
             const char* e = getenv("QUEST_PLAN_SEEDS");
             return e ? atoi(e) : 24;
         }();
+        const int maxSeeds = hooks && hooks->seeds > 0 ? hooks->seeds : maxSeedsEnv;
         int seeds = 0;
         u64 tried[16];
         int nTried = 0;

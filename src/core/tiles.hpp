@@ -177,6 +177,11 @@ struct PlanHooks {
     std::function<double(const TilePass&, const TileOp*)> passCost;
     double memCost = 0;
     double costMargin = 0.1;
+    // candidate passes seeded per pass (0: QUEST_PLAN_SEEDS, default 24) and
+    // the one-pass lookahead weight (< 0: QUEST_PLAN_LOOKAHEAD, default 0):
+    // knobs of the wave planner's strategy search (searchWavePlan)
+    int seeds = 0;
+    double lookahead = -1;
 };
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,

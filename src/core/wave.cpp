@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <thread>
 
 #include "router.hpp"
 
@@ -348,6 +349,68 @@ void waveCostHooks(PlanHooks& hooks) {
     hooks.passCost = [](const TilePass& ps, const TileOp* ops) { return wavePassCycles(ps, ops); };
     hooks.memCost = mem;
     hooks.costMargin = margin;
+}
+
+int searchWavePlan(const std::vector<Op>& ops, int L, int cdefault, PlanHooks& hooks, int* cmin) {
+    *cmin = cdefault;
+    static const bool on = !getenv("QUEST_PLAN_SEARCH") || atoi(getenv("QUEST_PLAN_SEARCH")) != 0;
+    static const size_t minOps = getenv("QUEST_PLAN_SEARCH_OPS") ? (size_t)atol(getenv("QUEST_PLAN_SEARCH_OPS")) : 256;
+    if (!on || ops.size() < minOps || L < kWaveBits + 6) return 0;
+    struct Strategy {
+        int dc;          // cmin - cdefault
+        int cost;        // compute-aware passes: 1 as waveCostHooks, 0 off, 2 without margin
+        int seeds;       // 0: default
+        double look;     // < 0: default
+    };
+    static const Strategy S[] = {{0, 1, 0, -1}, {1, 1, 0, -1}, {0, 0, 0, -1}, {1, 0, 0, -1},
+                                 {0, 2, 0, -1}, {0, 1, 48, -1}, {0, 1, 0, 0.5}};
+    constexpr int NS = (int)(sizeof S / sizeof S[0]);
+    PlanHooks costed;
+    waveCostHooks(costed);
+    const double M = costed.memCost > 0 ? costed.memCost : 12800.0;
+    auto apply = [&](const Strategy& st, PlanHooks& h) {
+        h.passCost = nullptr;
+        h.memCost = 0;
+        if (st.cost) {
+            h.passCost = [](const TilePass& ps, const TileOp* o) { return wavePassCycles(ps, o); };
+            h.memCost = M;
+            h.costMargin = st.cost == 2 ? 0.0 : costed.costMargin;
+        }
+        h.seeds = st.seeds;
+        h.lookahead = st.look;
+    };
+    double score[NS];
+    auto run = [&](int i) {
+        QuietPlan quiet;
+        const int c = cdefault + S[i].dc;
+        if (c >= kWaveBits - 1) {
+            score[i] = 1e300;
+            return;
+        }
+        PlanHooks h;
+        h.relabelOk = hooks.relabelOk;
+        h.lowPerm = hooks.lowPerm;
+        apply(S[i], h);
+        std::vector<Op> mine = ops;
+        TileProgram prog;
+        planTiles(mine, L, kWaveBits, c, true, prog, kWaveVecBits, &h);
+        double t = 0;
+        for (const TilePass& ps : prog.passes) {
+            const double cyc = wavePassCycles(ps, prog.ops.data() + ps.opBegin);
+            t += std::max(cyc < 0 ? M : cyc, M);
+        }
+        score[i] = t;
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < NS; i++) pool.emplace_back(run, i);
+    run(0);
+    for (std::thread& th : pool) th.join();
+    int best = 0;
+    for (int i = 1; i < NS; i++)
+        if (score[i] < score[best] * (1 - 1e-9)) best = i;
+    *cmin = cdefault + S[best].dc;
+    apply(S[best], hooks);
+    return best;
 }
 
 int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks) {

@@ -216,6 +216,17 @@ double wavePassCycles(const TilePass& ps, const TileOp* ops);
 // memCost / costMargin): QUEST_PLAN_MEM_CYCLES (0: off) and
 // QUEST_PLAN_COST_MARGIN.
 void waveCostHooks(PlanHooks& hooks);
+// Planner strategy search (QUEST_PLAN_SEARCH, default on): a queue of at least
+// QUEST_PLAN_SEARCH_OPS (256: the windows of programs that read the state rarely) plain wave ops is planned with several
+// strategies at once on worker threads (always-resident positions cdefault /
+// cdefault + 1, compute-aware passes on / off / without margin, more seed
+// candidates, one-pass lookahead; statistics untouched), each plan scored by
+// sum over passes of max(modeled compute, memory stream); *cmin and `hooks`
+// (the caller's, with the strategy's knobs set) then plan the kept strategy --
+// deterministically the same plan.  The greedy planner's pass count swings by
+// several passes from circuit to circuit with any single knob.  Returns the
+// index of the kept strategy (0: the default one).
+int searchWavePlan(const std::vector<Op>& ops, int L, int cdefault, PlanHooks& hooks, int* cmin);
 // Always-resident low positions for a relabelling wave plan of q.pending:
 // cdefault or cdefault + 1, whichever plans fewer passes (QUEST_WAVE_CMIN_SEARCH
 // =1; default: cdefault); sticky in q.waveCmin until the queue drains.

@@ -442,7 +442,9 @@ void flushImpl(QuregImpl& q, bool front) {
     if (relabel && !front) orig = q.pending;
     // as the HIP backend: 6 or 7 always-resident low positions, whichever
     // plans this queue in fewer passes
-    const int cminUse = (relabel && streamOn && !getenv("QUEST_WAVE_CMIN")) ? chooseWaveCmin(q, cminWave, hooks) : cminWave;
+    int cminUse = (relabel && streamOn && !getenv("QUEST_WAVE_CMIN")) ? chooseWaveCmin(q, cminWave, hooks) : cminWave;
+    // as the HIP backend: the strategy search on full flushes
+    if (relabel && streamOn && !front && !getenv("QUEST_WAVE_CMIN")) searchWavePlan(q.pending, q.L, cminUse, hooks, &cminUse);
     planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminUse : 4, rt().fusion, prog,
               relabel ? kWaveVecBits : -1, relabel && streamOn ? &hooks : nullptr);
     if (leftover.empty()) q.waveCmin = -1;   // the queue drained: choose afresh next time
