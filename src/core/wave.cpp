@@ -121,7 +121,9 @@ struct Scale {  // complex factor the pass still owes its amplitudes
 // LANTI; real: also M2R, M2RI, LM2R, LM2RI); else turn an unnormalised
 // Hadamard or a rotation back into a scaled M2R / M2RI; else append a phase op.
 void settleScale(WaveProgram& out, int begin, double sr, double si) {
-    auto free = [](const WaveOp& w) { return w.cReg == 0 && w.cLane == 0 && w.cLaneZero == 0 && w.ctrlOut == 0; };
+    auto free = [](const WaveOp& w) {
+        return w.cReg == 0 && w.cLane == 0 && w.cLaneZero == 0 && w.ctrlOut == 0 && w.ctrlOutZero == 0;
+    };
     const bool realF = si == 0;
     auto cm = [&](real* p) {  // p[0] + i p[1] *= (sr + i si)
         const double x = p[0] * sr - p[1] * si, y = p[0] * si + p[1] * sr;
@@ -769,7 +771,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         }
     };
     std::function<void(WaveOp)> emit = [&](WaveOp w) {
-        const bool free = w.cReg == 0 && w.cLane == 0 && w.cLaneZero == 0 && w.ctrlOut == 0;
+        const bool free = w.cReg == 0 && w.cLane == 0 && w.cLaneZero == 0 && w.ctrlOut == 0 && w.ctrlOutZero == 0;
         if (frameOn && free && w.kind == (int)WKind::SWAP && w.a >= VB) {
             F ^= 1u << lay.slotBit[w.a];
             return;
@@ -810,7 +812,8 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             else if (T) {
                 WaveOp rest = w;
                 rest.cReg &= ~T;
-                if (rest.cReg == 0 && rest.cLane == 0 && rest.cLaneZero == 0 && rest.ctrlOut == 0) {
+                if (rest.cReg == 0 && rest.cLane == 0 && rest.cLaneZero == 0 && rest.ctrlOut == 0 &&
+                    rest.ctrlOutZero == 0) {
                     double pr, pi;
                     phaseOf(rest, pr, pi);
                     sig.mul(pr, pi);   // a global factor: absorbed by the pass
@@ -1082,10 +1085,19 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         if (postClear) Cnd[postT] = 0;
         postT = -1;
     };
+    static const bool foldOn = !getenv("QUEST_WAVE_FOLD_DIAG") || atoi(getenv("QUEST_WAVE_FOLD_DIAG")) != 0;
+    // a real diagonal factor that is not a unit phase (those have cheap kinds)
+    auto foldable = [&](int x) {
+        const real* m = ops[x].m;
+        return foldOn && m[1] == 0 && m[0] != 0 && std::fabs((double)m[0]) != 1;
+    };
     for (int i = 0; i < nOps; i++) {
         if (cframeOn) {
             frameAfter();
-            if (frameBefore(i)) continue;
+            // a run of foldable diagonal ops resolves the frame itself (below)
+            const bool run = (OpKind)ops[i].kind == OpKind::Diag && foldable(i) && i + 1 < nOps &&
+                             (OpKind)ops[i + 1].kind == OpKind::Diag && foldable(i + 1);
+            if (!run && frameBefore(i)) continue;
         }
         const TileOp& op = ops[i];
         if (chan[i]) {
@@ -1104,6 +1116,63 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             w.m[4] = m[2 * 5];
             emit(w);
             continue;
+        }
+        if ((OpKind)op.kind == OpKind::Diag && foldable(i)) {
+            // A run of real diagonal factors (density dephasing lowered to
+            // diagonal ops: 15 per two-qubit channel, most of their masks
+            // partly or wholly outside the tile): group the run's ops by their
+            // in-tile mask; per group the out-of-tile bits U of its ops take
+            // 2^|U| values, so ONE op per value carries the product of the
+            // group's factors for it (ctrlOut = the 1 bits, ctrlOutZero = the
+            // 0 bits) -- each tile executes at most one op per group instead of
+            // every op whose outside bits it matches.  QUEST_WAVE_FOLD_DIAG=0 off.
+            int j = i;
+            while (j < nOps && (OpKind)ops[j].kind == OpKind::Diag && foldable(j)) j++;
+            if (j - i >= 2) {
+                for (int x = i; x < j; x++)
+                    for (unsigned b = ops[x].ctrlIn; b; b &= b - 1)
+                        if (cframeOn && Cnd[__builtin_ctz(b)]) execConds(x, __builtin_ctz(b));
+                std::vector<unsigned> masksIn;
+                for (int x = i; x < j; x++)
+                    if (std::find(masksIn.begin(), masksIn.end(), ops[x].ctrlIn) == masksIn.end())
+                        masksIn.push_back(ops[x].ctrlIn);
+                for (unsigned mi : masksIn) {
+                    u64 U = 0;
+                    for (int x = i; x < j; x++)
+                        if (ops[x].ctrlIn == mi) U |= ops[x].ctrlOut;
+                    const int nu = __builtin_popcountll(U);
+                    if (nu > 3) {   // too many combinations: the ops as they are
+                        for (int x = i; x < j; x++) {
+                            if (ops[x].ctrlIn != mi) continue;
+                            WaveOp w = blank((int)WKind::DIAG);
+                            masks(lay, mi, w.cReg, w.cLane);
+                            w.ctrlOut = ops[x].ctrlOut;
+                            w.m[0] = ops[x].m[0];
+                            emit(w);
+                        }
+                        continue;
+                    }
+                    int ub[3], k = 0;
+                    for (u64 u = U; u; u &= u - 1) ub[k++] = __builtin_ctzll(u);
+                    for (int v = 0; v < (1 << nu); v++) {
+                        u64 one = 0;
+                        for (int q = 0; q < nu; q++)
+                            if ((v >> q) & 1) one |= 1ull << ub[q];
+                        double f = 1;
+                        for (int x = i; x < j; x++)
+                            if (ops[x].ctrlIn == mi && (ops[x].ctrlOut & ~one) == 0) f *= ops[x].m[0];
+                        if (f == 1) continue;
+                        WaveOp w = blank((int)WKind::DIAG);
+                        masks(lay, mi, w.cReg, w.cLane);
+                        w.ctrlOut = one;
+                        w.ctrlOutZero = U & ~one;
+                        w.m[0] = (real)f;
+                        emit(w);
+                    }
+                }
+                i = j - 1;
+                continue;
+            }
         }
         if ((OpKind)op.kind == OpKind::Diag) {
             if (emitPhase(op.ctrlIn, op, op.m[0], op.m[1])) continue;

@@ -125,6 +125,7 @@ struct WaveOp {
     // lane L when ((L ^ fLane) & cLane) == cLane (real lane bits)
     unsigned fReg, fLane;
     u64 ctrlOut;      // physical bits outside the tile that must be 1
+    u64 ctrlOutZero;  // ... that must be 0 (DIAG only: folded diagonal runs, planWavePass)
     real m[8];
 };
 

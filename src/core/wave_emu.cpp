@@ -322,7 +322,7 @@ void emulateWavePass(real* re, real* im, int L, const WaveProgram& wp, const Wav
                     }
                 for (int o = ps.opBegin; o < ps.opEnd; o++) {
                     const WaveOp& w = wp.ops[o];
-                    if (((u64)base & w.ctrlOut) != w.ctrlOut) continue;
+                    if (((u64)base & w.ctrlOut) != w.ctrlOut || ((u64)base & w.ctrlOutZero)) continue;
                     applyWaveOp(w, vr, vi);
                 }
                 for (int lane = g * per; lane < (g + 1) * per; lane++)

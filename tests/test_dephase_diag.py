@@ -96,3 +96,72 @@ def test_fp32_dephasing_leaves_populations_untouched():
     out = subprocess.run([sys.executable, "-c", FP32_POPS], cwd=root, env=env, capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+
+
+FOLD = r'''
+import sys
+import numpy as np
+import quest_amd as qa
+from quest_amd.ops import capi
+from quest_amd.utils import oracle as O
+n = 10
+e = qa.Env()
+r = qa.Register(e, n, density=True)
+rng = np.random.default_rng(5)
+psi = rng.normal(size=1 << n) + 1j * rng.normal(size=1 << n)
+psi /= np.linalg.norm(psi)
+rho = np.outer(psi, psi.conj())
+r.set_amps(rho.flatten(order="F"))
+o = O.DensityMatrix(n, rho.copy())
+r.sync()
+capi.resetQuESTStats()
+for a in range(0, n - 1, 2):
+    r.dephase2(a, a + 1, 0.3); o.dephase2(a, a + 1, 0.3)
+for q in (1, 4, 8):
+    r.dephase(q, 0.2); o.dephase(q, 0.2)
+r.h(3); o.apply(np.array([[1, 1], [1, -1]]) / np.sqrt(2), 3)
+for a in range(1, n - 1, 2):
+    r.dephase2(a, a + 1, 0.45); o.dephase2(a, a + 1, 0.45)
+r.sync()
+st = capi.getQuESTStats()
+got = r.to_numpy().reshape(1 << n, 1 << n, order="F")
+err = np.max(np.abs(got - o.rho))
+print("fold err", err, "passes", st["passes"], "wave", st["wavePasses"], "waveOps", st["waveOps"])
+assert err < 1e-12, err
+assert st["wavePasses"] == st["passes"] >= 1, st
+'''
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
+def test_folded_diagonal_runs_on_the_wave_planner(fold):
+    """Runs of dephasing factors (diagonal ops whose masks lie partly or wholly
+    outside the tile) folded per in-tile mask into one op per value of their
+    outside bits (ctrlOut / ctrlOutZero), on the wave planner's host emulation
+    of a 10-qubit density matrix, against the Kraus oracle;
+    QUEST_WAVE_FOLD_DIAG=0 emits every op."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QUEST_BACKEND="cpu", QUEST_CPU_PLANNER="3", QUEST_WAVE_FOLD_DIAG=fold)
+    out = subprocess.run([sys.executable, "-c", FOLD], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "fold err" in out.stdout
+
+
+@pytest.mark.gpu
+def test_folded_diagonal_runs_gpu():
+    """The same on the GPU kernel (check path with out-of-tile zero bits)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = FOLD.replace("n = 10", "n = 11")
+    env = dict(os.environ, QUEST_BACKEND="hip")
+    out = subprocess.run([sys.executable, "-c", script], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "fold err" in out.stdout

@@ -44,7 +44,7 @@ def test_quad_library_is_long_double():
 
 def test_quad_gate_channel_marginal_suites():
     env = dict(os.environ, QUEST_PREC="4", QUEST_BACKEND="cpu")
-    out = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+    out = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu",
                           "tests/test_gates.py", "tests/test_chan2_gates.py", "tests/test_dephase_diag.py",
                           "tests/test_marginals.py", "tests/test_validation.py"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)

@@ -409,6 +409,14 @@ class Gen:
         e("s_and_b64 s[96:97], s[32:33], s[40:41]")    # ctrlOut of the op
         e("s_cmp_eq_u64 s[96:97], s[40:41]")
         e("s_cbranch_scc0 .Lskip_op")
+        # handler bit 30: out-of-tile bits that must be 0 in record bytes
+        # 48-55 (a DIAG's spare m[2]; folded diagonal runs)
+        e("s_bitcmp1_b32 s36, 30")
+        e("s_cbranch_scc0 .Lcheck_zero_done")
+        e("s_and_b64 s[96:97], s[32:33], s[48:49]")
+        e("s_cmp_eq_u64 s[96:97], 0")
+        e("s_cbranch_scc0 .Lskip_op")
+        self.label(".Lcheck_zero_done")
         if self.W:
             e("s_and_b32 s96, s3, s42")                 # wave bits that must be 1
             e("s_cmp_eq_u32 s96, s42")
@@ -417,6 +425,7 @@ class Gen:
             e("s_cmp_eq_u32 s96, 0")
             e("s_cbranch_scc0 .Lskip_op")
         e("s_bitset0_b32 s36, 31")
+        e("s_bitset0_b32 s36, 30")
         e("s_add_u32 s98, s92, s36")
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
