@@ -52,6 +52,9 @@ void exchange(const Xfer* x, int n);
 // (0 or 1).  Stream-less transports finish inside exchangeAsync.
 void exchangeAsync(const Xfer* x, int n, int slot);
 void exchangeWait(int slot);
+// Whether the transport can send from any device memory (RCCL: the state
+// itself), not only from comm buffers (IPC exports them, sockets stage them).
+bool sendsFromState();
 // In-place sum of host doubles across ranks.
 void allreduceSum(double* vals, int n);
 // In-place logical AND of a host int across ranks.

@@ -24,6 +24,7 @@ void exchange(const Xfer* x, int n) {
     for (int i = 0; i < n; i++) sock::sendrecv(x[i].peer, x[i].send, x[i].recv, x[i].bytes);
 }
 void exchangeAsync(const Xfer* x, int n, int) { exchange(x, n); }
+bool sendsFromState() { return false; }
 void exchangeWait(int) {}
 void allreduceSum(double* vals, int n) { sock::allreduceSum(vals, n); }
 int allreduceAnd(int v) {

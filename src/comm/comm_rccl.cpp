@@ -361,6 +361,8 @@ void exchange(const Xfer* x, int n) {
     deviceExchange(x, n, 0, S(), S());
 }
 
+bool sendsFromState() { return g_mode == Mode::Rccl; }
+
 bool pipelined() {
     static const bool off = getenv("QUEST_EXCHANGE_PIPELINE") && atoi(getenv("QUEST_EXCHANGE_PIPELINE")) == 0;
     return !off && (g_mode == Mode::Rccl || g_mode == Mode::Ipc) && g_cstream;

@@ -304,3 +304,31 @@ def restore_chunks(env):
 
 
 SCENARIOS["restore_chunks"] = restore_chunks
+
+
+def top_swap(env):
+    """Gates on qubits 0-5 and 7 of 8, qubit 6 idle: on 2 ranks the swap that
+    brings rank qubit 7 in takes qubit 6, the top local position, so each
+    part of the chunk is one contiguous range and RCCL sends it straight
+    from the state (router multiSwap, no pack)."""
+    import quest_amd as qa
+    from quest_amd.ops import capi
+
+    n = 8
+    r = qa.Register(env, n)
+    r.init_plus()
+    rng = np.random.default_rng(9)
+    capi.resetQuESTStats()
+    for layer in range(3):
+        for q in (0, 1, 2, 3, 4, 5, 7):
+            r.ry(q, float(rng.uniform(0, 3)))
+            r.rz(q, float(rng.uniform(0, 3)))
+        for a in range(0, 5, 2):
+            r.cnot(a, a + 1)
+        r.cnot(5, 7)
+    out = {"state": r.to_numpy(), "probs": np.array([r.prob(q, 1) for q in range(n)])}
+    r.close()
+    return out
+
+
+SCENARIOS["top_swap"] = top_swap

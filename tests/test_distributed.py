@@ -36,7 +36,7 @@ def _multi(name, ranks, tmp_path, **env):
 
 @pytest.mark.parametrize("ranks", [2, 4])
 @pytest.mark.parametrize("name", ["random_ops_statevector", "random_ops_density", "measurement_and_collapse",
-                                  "calculations", "qasm_log"])
+                                  "calculations", "qasm_log", "top_swap"])
 def test_distributed_equivalence(env, tmp_path, name, ranks):
     want = _single(name, env)
     got = _multi(name, ranks, tmp_path)

@@ -298,7 +298,7 @@ def test_reference_golden_suite_on_gpu(genv):
 
 
 _DIST = ["random_ops_statevector", "random_ops_density", "measurement_and_collapse", "calculations", "qasm_log",
-         "rank_qubit_gates"]
+         "rank_qubit_gates", "top_swap"]
 
 
 @pytest.mark.parametrize("transport,ranks,slice_kb", [("ipc", 2, ""), ("ipc", 4, ""), ("ipc", 4, "1"),
