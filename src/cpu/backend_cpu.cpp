@@ -413,8 +413,18 @@ void flushImpl(QuregImpl& q, bool front) {
     static const int waveCmin = getenv("QUEST_WAVE_CMIN") ? atoi(getenv("QUEST_WAVE_CMIN")) : kWaveVecBits + 5;  // as the HIP backend
     bool channels = false;   // as the HIP backend: density-channel flushes keep one low position fewer
     for (const Op& op : q.pending) channels = channels || op.kind == OpKind::Mat4 || op.kind == OpKind::DensChan2;
-    const int cminWave = channels ? kWaveVecBits + 4 : waveCmin;
-    const bool relabel = wave && !channels && rt().fusion && waveRelabel() && !rt().verify;
+    // (QUEST_WAVE_CMIN_CHAN: the always-resident low positions of channel
+    // flushes, kWaveVecBits + 3 .. kWaveBits - 2; the density damping trade)
+    static const int cminChan = [] {
+        const char* e = getenv("QUEST_WAVE_CMIN_CHAN");
+        return e ? std::max(kWaveVecBits + 3, std::min(atoi(e), kWaveBits - 2)) : kWaveVecBits + 4;
+    }();
+    const int cminWave = channels ? cminChan : waveCmin;
+    // QUEST_WAVE_CHAN_RELABEL=1: channel flushes relabel too (a channel needs
+    // its row and column bits in one tile; relabelling lets the low positions
+    // hold different qubits pass by pass)
+    static const bool chanRelabel = getenv("QUEST_WAVE_CHAN_RELABEL") && atoi(getenv("QUEST_WAVE_CHAN_RELABEL")) != 0;
+    const bool relabel = wave && (!channels || chanRelabel) && rt().fusion && waveRelabel() && !rt().verify;
     // as the HIP backend (streamed wave flushes): relabel only passes the wave
     // engine lowers -- the same plans (QUEST_PLAN_STREAM=0: the fallback below)
     static const bool streamOn = !getenv("QUEST_PLAN_STREAM") || atoi(getenv("QUEST_PLAN_STREAM")) != 0;

@@ -137,3 +137,46 @@ def test_channel_op_fallback():
     out = subprocess.run([sys.executable, "-c", FALLBACK, ROOT], cwd=ROOT, env=env, capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+
+
+CHAN_RELABEL = r'''
+import numpy as np
+import quest_amd as qa
+from quest_amd.ops import capi
+from quest_amd.utils import oracle as O
+n = 10
+e = qa.Env()
+r = qa.Register(e, n, density=True)
+rng = np.random.default_rng(12)
+rho = O.random_density(rng, n)
+r.set_amps(rho.flatten(order="F"))
+o = O.DensityMatrix(n, rho.copy())
+H = np.array([[1, 1], [1, -1]]) / np.sqrt(2)
+for rep in range(2):
+    for q in range(n):
+        r.damping(q, 0.1 + 0.02 * q); o.damping(q, 0.1 + 0.02 * q)
+    for q in range(0, n, 3):
+        r.h(q); o.apply(H, q)
+    for q in range(n):
+        r.depolarise(q, 0.05); o.depolarise(q, 0.05)
+r.sync()
+st = capi.getQuESTStats()
+got = r.to_numpy().reshape(1 << n, 1 << n, order="F")
+err = np.max(np.abs(got - o.rho))
+print("chan relabel err", err, "passes", st["passes"], "wave", st["wavePasses"])
+assert err < 1e-12, err
+'''
+
+
+@pytest.mark.parametrize("relabel,cmin", [("1", "4"), ("1", "5"), ("0", "4")])
+def test_channel_flush_relabelling(relabel, cmin):
+    """One-qubit damping / depolarising (register channels CH1 on row and
+    column bits) in flushes that relabel (QUEST_WAVE_CHAN_RELABEL=1) and keep
+    fewer always-resident positions (QUEST_WAVE_CMIN_CHAN), on the wave
+    planner's host emulation against the Kraus oracle."""
+    env = dict(os.environ, QUEST_BACKEND="cpu", QUEST_CPU_PLANNER="3", QUEST_WAVE_CHAN_RELABEL=relabel,
+               QUEST_WAVE_CMIN_CHAN=cmin)
+    out = subprocess.run([sys.executable, "-c", CHAN_RELABEL], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "chan relabel err" in out.stdout
