@@ -733,12 +733,19 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         for (int l = 0; l < kWaveLaneBits; l++) m |= ((F >> lay.laneBit[l]) & 1u) << l;
         return m;
     };
+    // conditional flips (deferred CNOTs, see below); declared here because a
+    // physical X on a condition bit toggles its dependents' flips
+    unsigned Cnd[kWaveBits] = {0};
     auto materialize = [&](unsigned slots) {
         for (unsigned m = slots & slotFlips(); m; m &= m - 1) {
             WaveOp x = blank((int)WKind::SWAP);
             x.a = __builtin_ctz(m);
             out.ops.push_back(x);
-            F &= ~(1u << lay.slotBit[x.a]);
+            const int b = lay.slotBit[x.a];
+            F &= ~(1u << b);
+            // x_t = p_t ^ F_t ^ p_b for t conditioned on b: p_b just flipped
+            for (int t = 0; t < kWaveBits; t++)
+                if ((Cnd[t] >> b) & 1u) F ^= 1u << t;
         }
     };
     // the unit phase p of a phase op (DIAG: its complex factor)
@@ -960,7 +967,6 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // op needs it; at the end of the pass the flips whose target and
     // conditions are in one domain (slots, real lanes, wave bits) are folded
     // into the store maps (WavePass::stCondSlot / stCondLane).
-    unsigned Cnd[kWaveBits] = {0};
     auto deps = [&](int c) {
         unsigned m = 0;
         for (int u = 0; u < kWaveBits; u++) m |= ((Cnd[u] >> c) & 1u) << u;

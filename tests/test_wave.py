@@ -141,6 +141,64 @@ assert err < 1e-10, err
 '''
 
 
+CFRAME = r'''
+import os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import quest_amd as qa
+from helpers import GATES_1Q, GATES_2Q, GATES_MQ, apply_named, oracle_for, random_qubits
+
+env = qa.Env()
+n = int(sys.argv[3])
+rng = np.random.default_rng(int(sys.argv[2]))
+r = qa.Register(env, n)
+o = oracle_for(r, rng)
+names = GATES_1Q + GATES_2Q + GATES_MQ
+for step in range(250):
+    # a CNOT (deferred as a conditional flip), then gates on / controlled by /
+    # phased on its control or target -- X and Y on the control toggle flips
+    c, t = random_qubits(rng, n, 2)
+    apply_named(r, o, "cnot", [c, t], rng)
+    for _ in range(int(rng.integers(1, 4))):
+        q = c if rng.random() < 0.5 else t
+        if rng.random() < 0.3:
+            apply_named(r, o, ["x", "y", "z"][int(rng.integers(3))], [q], rng)
+            continue
+        name = names[rng.integers(len(names))]
+        k = 1 if name in GATES_1Q else 2 if name in GATES_2Q else int(rng.integers(2, 5))
+        qs = random_qubits(rng, n, k)
+        if q not in qs:
+            qs[int(rng.integers(k))] = q
+        apply_named(r, o, name, qs, rng)
+err = np.max(np.abs(r.to_numpy() - o.v))
+print("cframe err", err)
+assert err < 1e-10, err
+'''
+
+
+@pytest.mark.parametrize("cframe", ["1", "0"])
+def test_conditional_frame_emulated_on_host(cframe):
+    """Deferred CNOTs (planWavePass conditional flips): each CNOT followed by
+    gates that use its control or target as target, control or phase mask,
+    and X / Y / Z on them (a physical X on an exchanged condition bit must
+    toggle the flips it conditions -- the 30-qubit GPU failure of round 4), on
+    the wave planner's host emulation against the NumPy oracle;
+    QUEST_WAVE_CFRAME=0 executes every CNOT."""
+    for seed, n in ((1, 16), (2, 20), (3, 20)):
+        out = _run(["-c", CFRAME, ROOT, str(seed), str(n)],
+                   {"QUEST_BACKEND": "cpu", "QUEST_CPU_PLANNER": "3", "QUEST_WAVE_CFRAME": cframe})
+        assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+        assert "cframe err" in out.stdout
+
+
+@pytest.mark.gpu
+def test_conditional_frame_gpu():
+    """The conditional-frame stress on the GPU kernel (22 qubits)."""
+    out = _run(["-c", CFRAME, ROOT, "4", "22"], {"QUEST_BACKEND": "hip"}, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert "cframe err" in out.stdout
+
+
 @pytest.mark.parametrize("frame", ["1", "0"])
 def test_exchange_frame_emulated_on_host(frame):
     """Deferred X gates (planWavePass exchange frame): X on random qubits
