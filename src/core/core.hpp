@@ -16,6 +16,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <future>
 #include <vector>
 
 namespace qa {
@@ -94,6 +95,11 @@ struct QuregImpl {
     // wave planner: always-resident low positions chosen for the ops queued
     // now (chooseWaveCmin), kept until the queue has drained (-1: not chosen)
     int waveCmin = -1;
+    // wave planner strategy for this queue's front flushes (searchWaveStrategy,
+    // run in the background after the window's first front flush; -1: the
+    // default), kept until the queue has drained
+    int planStrategy = -1;
+    std::future<int> strategySearch;
     bool permIdentity() const {
         for (int i = 0; i < nSV; i++)
             if (l2p[i] != i) return false;

@@ -275,7 +275,7 @@ int& planMaxOps() {
 }
 
 int& fuseBlockQubits() {
-    static int q = 2;
+    static thread_local int q = 2;   // per thread: planner worker threads set their own
     return q;
 }
 

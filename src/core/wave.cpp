@@ -285,6 +285,7 @@ bool relabelsLower(const TileProgram& prog) {
 
 long long g_waveStoreTrCost = 0;
 thread_local int t_planQuiet = 0;
+thread_local int t_waveCframe = -1;
 
 bool waveLowers(const TilePass& ps, const TileOp* ops) {
     QuietPlan quiet;
@@ -353,66 +354,103 @@ void waveCostHooks(PlanHooks& hooks) {
     hooks.costMargin = margin;
 }
 
-int searchWavePlan(const std::vector<Op>& ops, int L, int cdefault, PlanHooks& hooks, int* cmin) {
-    *cmin = cdefault;
-    static const bool on = !getenv("QUEST_PLAN_SEARCH") || atoi(getenv("QUEST_PLAN_SEARCH")) != 0;
-    static const size_t minOps = getenv("QUEST_PLAN_SEARCH_OPS") ? (size_t)atol(getenv("QUEST_PLAN_SEARCH_OPS")) : 256;
-    if (!on || ops.size() < minOps || L < kWaveBits + 6) return 0;
-    struct Strategy {
-        int dc;          // cmin - cdefault
-        int cost;        // compute-aware passes: 1 as waveCostHooks, 0 off, 2 without margin
-        int seeds;       // 0: default
-        double look;     // < 0: default
-    };
-    static const Strategy S[] = {{0, 1, 0, -1}, {1, 1, 0, -1}, {0, 0, 0, -1}, {1, 0, 0, -1},
-                                 {0, 2, 0, -1}, {0, 1, 48, -1}, {0, 1, 0, 0.5}};
-    constexpr int NS = (int)(sizeof S / sizeof S[0]);
+namespace {
+struct WaveStrategy {
+    int dc;        // always-resident low positions - cdefault
+    int cost;      // compute-aware passes: 1 as waveCostHooks, 0 off, 2 without margin
+    int seeds;     // seed candidates per pass (0: default)
+    double look;   // one-pass lookahead weight (< 0: default)
+    int cframe;    // conditional exchange frame: 1 as configured, 0 off
+};
+// 0 is the default; the last one is the round-3 planner (no compute-aware
+// passes, no conditional frame)
+const WaveStrategy kStrategies[] = {{0, 1, 0, -1, 1}, {1, 1, 0, -1, 1}, {0, 0, 0, -1, 1}, {1, 0, 0, -1, 1},
+                                    {0, 2, 0, -1, 1}, {0, 1, 48, -1, 1}, {0, 1, 0, 0.5, 1}, {0, 0, 0, -1, 0}};
+constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
+
+void strategyHooks(const WaveStrategy& st, PlanHooks& h) {
     PlanHooks costed;
     waveCostHooks(costed);
     const double M = costed.memCost > 0 ? costed.memCost : 12800.0;
-    auto apply = [&](const Strategy& st, PlanHooks& h) {
-        h.passCost = nullptr;
-        h.memCost = 0;
-        if (st.cost) {
-            h.passCost = [](const TilePass& ps, const TileOp* o) { return wavePassCycles(ps, o); };
-            h.memCost = M;
-            h.costMargin = st.cost == 2 ? 0.0 : costed.costMargin;
-        }
-        h.seeds = st.seeds;
-        h.lookahead = st.look;
-    };
-    double score[NS];
+    h.passCost = nullptr;
+    h.memCost = 0;
+    if (st.cost) {
+        h.passCost = [](const TilePass& ps, const TileOp* o) { return wavePassCycles(ps, o); };
+        h.memCost = M;
+        h.costMargin = st.cost == 2 ? 0.0 : costed.costMargin;
+    }
+    h.seeds = st.seeds;
+    h.lookahead = st.look;
+}
+}  // namespace
+
+size_t waveSearchMinOps() {
+    static const size_t v = getenv("QUEST_PLAN_SEARCH_OPS") ? (size_t)atol(getenv("QUEST_PLAN_SEARCH_OPS")) : 256;
+    return v;
+}
+
+bool waveFrontSearch() {
+    static const bool v = !getenv("QUEST_PLAN_SEARCH_FRONT") || atoi(getenv("QUEST_PLAN_SEARCH_FRONT")) != 0;
+    return v;
+}
+
+int waveFrontStrategy() {
+    static const int v = getenv("QUEST_PLAN_FRONT_STRATEGY") ? atoi(getenv("QUEST_PLAN_FRONT_STRATEGY")) : 0;
+    return v;
+}
+
+int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const PlanHooks& base) {
+    static const bool on = !getenv("QUEST_PLAN_SEARCH") || atoi(getenv("QUEST_PLAN_SEARCH")) != 0;
+    if (!on || ops.size() < waveSearchMinOps() || L < kWaveBits + 6) return -1;
+    PlanHooks costed;
+    waveCostHooks(costed);
+    const double M = costed.memCost > 0 ? costed.memCost : 12800.0;
+    const int fuse = fuseBlockQubits();
+    double score[kNumStrategies];
     auto run = [&](int i) {
         QuietPlan quiet;
-        const int c = cdefault + S[i].dc;
-        if (c >= kWaveBits - 1) {
-            score[i] = 1e300;
-            return;
+        fuseBlockQubits() = fuse;              // (thread-local)
+        t_waveCframe = kStrategies[i].cframe;  // (thread-local)
+        const int c = cdefault + kStrategies[i].dc;
+        score[i] = 1e300;
+        if (c < kWaveBits - 1) {
+            PlanHooks h;
+            h.relabelOk = base.relabelOk;
+            h.lowPerm = base.lowPerm;
+            strategyHooks(kStrategies[i], h);
+            std::vector<Op> mine = ops;
+            TileProgram prog;
+            planTiles(mine, L, kWaveBits, c, true, prog, kWaveVecBits, &h);
+            double t = 0;
+            for (const TilePass& ps : prog.passes) {
+                const double cyc = wavePassCycles(ps, prog.ops.data() + ps.opBegin);
+                t += std::max(cyc < 0 ? M : cyc, M);
+            }
+            score[i] = t;
         }
-        PlanHooks h;
-        h.relabelOk = hooks.relabelOk;
-        h.lowPerm = hooks.lowPerm;
-        apply(S[i], h);
-        std::vector<Op> mine = ops;
-        TileProgram prog;
-        planTiles(mine, L, kWaveBits, c, true, prog, kWaveVecBits, &h);
-        double t = 0;
-        for (const TilePass& ps : prog.passes) {
-            const double cyc = wavePassCycles(ps, prog.ops.data() + ps.opBegin);
-            t += std::max(cyc < 0 ? M : cyc, M);
-        }
-        score[i] = t;
+        t_waveCframe = -1;
     };
     std::vector<std::thread> pool;
-    for (int i = 1; i < NS; i++) pool.emplace_back(run, i);
+    for (int i = 1; i < kNumStrategies; i++) pool.emplace_back(run, i);
     run(0);
     for (std::thread& th : pool) th.join();
     int best = 0;
-    for (int i = 1; i < NS; i++)
+    for (int i = 1; i < kNumStrategies; i++)
         if (score[i] < score[best] * (1 - 1e-9)) best = i;
-    *cmin = cdefault + S[best].dc;
-    apply(S[best], hooks);
     return best;
+}
+
+WaveStrategyScope::WaveStrategyScope(int idx, int cdefault, PlanHooks& hooks, int* cmin) {
+    *cmin = cdefault;
+    if (idx < 0 || idx >= kNumStrategies) return;
+    *cmin = cdefault + kStrategies[idx].dc;
+    strategyHooks(kStrategies[idx], hooks);
+    t_waveCframe = kStrategies[idx].cframe;
+    active = true;
+}
+
+WaveStrategyScope::~WaveStrategyScope() {
+    if (active) t_waveCframe = -1;
 }
 
 int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks) {
@@ -594,8 +632,10 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // exchange frame below): a CNOT with one control inside the tile and no
     // control outside is not executed either -- its target is marked flipped
     // where its control is 1 (see Cnd below), so it needs no register slot
-    static const bool cframeOn = (!getenv("QUEST_WAVE_XFRAME") || atoi(getenv("QUEST_WAVE_XFRAME")) != 0) &&
-                                 (!getenv("QUEST_WAVE_CFRAME") || atoi(getenv("QUEST_WAVE_CFRAME")) != 0);
+    static const bool xframeEnv = !getenv("QUEST_WAVE_XFRAME") || atoi(getenv("QUEST_WAVE_XFRAME")) != 0;
+    static const bool cframeEnv = xframeEnv && (!getenv("QUEST_WAVE_CFRAME") || atoi(getenv("QUEST_WAVE_CFRAME")) != 0);
+    // a planner strategy may switch it off for the flush it plans (t_waveCframe)
+    const bool cframeOn = t_waveCframe >= 0 ? (xframeEnv && t_waveCframe != 0) : cframeEnv;
     auto deferCnot = [&](int i) {
         const TileOp& op = ops[i];
         return cframeOn && (OpKind)op.kind == OpKind::Mat2 && cls[i] == M2Class::Swap && op.ctrlOut == 0 &&

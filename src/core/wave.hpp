@@ -217,17 +217,35 @@ double wavePassCycles(const TilePass& ps, const TileOp* ops);
 // memCost / costMargin): QUEST_PLAN_MEM_CYCLES (0: off) and
 // QUEST_PLAN_COST_MARGIN.
 void waveCostHooks(PlanHooks& hooks);
-// Planner strategy search (QUEST_PLAN_SEARCH, default on): a queue of at least
-// QUEST_PLAN_SEARCH_OPS (256: the windows of programs that read the state rarely) plain wave ops is planned with several
-// strategies at once on worker threads (always-resident positions cdefault /
-// cdefault + 1, compute-aware passes on / off / without margin, more seed
-// candidates, one-pass lookahead; statistics untouched), each plan scored by
-// sum over passes of max(modeled compute, memory stream); *cmin and `hooks`
-// (the caller's, with the strategy's knobs set) then plan the kept strategy --
-// deterministically the same plan.  The greedy planner's pass count swings by
-// several passes from circuit to circuit with any single knob.  Returns the
-// index of the kept strategy (0: the default one).
-int searchWavePlan(const std::vector<Op>& ops, int L, int cdefault, PlanHooks& hooks, int* cmin);
+// Planner strategy search (QUEST_PLAN_SEARCH, default on).  The greedy
+// planner's pass count swings by several passes from circuit to circuit with
+// any single knob; searchWaveStrategy plans a queue of at least
+// QUEST_PLAN_SEARCH_OPS (256) plain wave ops with every strategy at once on
+// worker threads (always-resident positions cdefault / cdefault + 1,
+// compute-aware passes on / off / without margin, more seed candidates,
+// one-pass lookahead, and the round-3 planner without the conditional frame;
+// statistics untouched), scores each plan by sum over passes of max(modeled
+// compute, memory stream) and returns the best one's index (-1: no search).
+// Thread-safe: the backends run it synchronously (worker threads) on full
+// flushes and in the background after a window's first front flush.
+int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const PlanHooks& base);
+size_t waveSearchMinOps();
+// QUEST_PLAN_SEARCH_FRONT=0: no background search after front flushes;
+// QUEST_PLAN_FRONT_STRATEGY: the strategy of front flushes until a search
+// has chosen one (default 0)
+bool waveFrontSearch();
+int waveFrontStrategy();
+// Plan (and lower) a flush with strategy idx (< 0: the default): sets the
+// hooks' knobs and *cmin, and the thread's conditional-frame switch until
+// the scope ends -- the lowering of the streamed passes must see the planner's.
+struct WaveStrategyScope {
+    WaveStrategyScope(int idx, int cdefault, PlanHooks& hooks, int* cmin);
+    ~WaveStrategyScope();
+    WaveStrategyScope(const WaveStrategyScope&) = delete;
+    WaveStrategyScope& operator=(const WaveStrategyScope&) = delete;
+    bool active = false;
+};
+extern thread_local int t_waveCframe;   // conditional frame of this thread's plans: -1 env, 0 off, 1 on
 // Always-resident low positions for a relabelling wave plan of q.pending:
 // cdefault or cdefault + 1, whichever plans fewer passes (QUEST_WAVE_CMIN_SEARCH
 // =1; default: cdefault); sticky in q.waveCmin until the queue drains.

@@ -453,11 +453,36 @@ void flushImpl(QuregImpl& q, bool front) {
     // as the HIP backend: 6 or 7 always-resident low positions, whichever
     // plans this queue in fewer passes
     int cminUse = (relabel && streamOn && !getenv("QUEST_WAVE_CMIN")) ? chooseWaveCmin(q, cminWave, hooks) : cminWave;
-    // as the HIP backend: the strategy search on full flushes
-    if (relabel && streamOn && !front && !getenv("QUEST_WAVE_CMIN")) searchWavePlan(q.pending, q.L, cminUse, hooks, &cminUse);
+    // Strategy search (searchWaveStrategy): full flushes search their own
+    // queue on worker threads while the GPU works through the passes the front
+    // flushes launched; front flushes use the strategy a background search
+    // picked from the queue left after the window's first front flush (the
+    // default until then).  Deterministic: a choice depends on queues only.
+    const bool searchable = relabel && streamOn && !getenv("QUEST_WAVE_CMIN");
+    int strategy = -1;
+    if (searchable) {
+        if (q.strategySearch.valid()) q.planStrategy = q.strategySearch.get();
+        strategy = front ? (q.planStrategy >= 0 ? q.planStrategy : waveFrontStrategy())
+                         : searchWaveStrategy(q.pending, q.L, cminUse, hooks);
+    }
+    const int cminBase = cminUse;
+    WaveStrategyScope strategyScope(strategy, cminBase, hooks, &cminUse);
     planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminUse : 4, rt().fusion, prog,
               relabel ? kWaveVecBits : -1, relabel && streamOn ? &hooks : nullptr);
-    if (leftover.empty()) q.waveCmin = -1;   // the queue drained: choose afresh next time
+    if (leftover.empty()) {   // the queue drained: choose afresh next time
+        q.waveCmin = -1;
+        q.planStrategy = -1;
+    } else if (front && searchable && waveFrontSearch() && q.planStrategy < 0 && !q.strategySearch.valid() &&
+               leftover.size() >= waveSearchMinOps()) {
+        PlanHooks base;
+        base.relabelOk = hooks.relabelOk;
+        base.lowPerm = hooks.lowPerm;
+        q.strategySearch = std::async(std::launch::async, [ops = leftover, L = q.L, c = cminBase, base,
+                                                           fuse = fuseBlockQubits()]() {
+            fuseBlockQubits() = fuse;   // (thread-local: this flush's setting)
+            return std::max(0, searchWaveStrategy(ops, L, c, base));
+        });
+    }
     if (!front && relabel && programRelabels(prog) && !relabelsLower(prog)) {
         q.pending.swap(orig);
         planTiles(q.pending, q.L, kWaveBits, cminWave, rt().fusion, prog);
