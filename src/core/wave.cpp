@@ -362,16 +362,25 @@ struct WaveStrategy {
     double look;   // one-pass lookahead weight (< 0: default)
     int cframe;    // conditional exchange frame: 1 as configured, 0 off
 };
-// 0 is the default; the last one is the round-3 planner (no compute-aware
-// passes, no conditional frame)
-const WaveStrategy kStrategies[] = {{0, 1, 0, -1, 1}, {1, 1, 0, -1, 1}, {0, 0, 0, -1, 1}, {1, 0, 0, -1, 1},
-                                    {0, 2, 0, -1, 1}, {0, 1, 48, -1, 1}, {0, 1, 0, 0.5, 1}, {0, 0, 0, -1, 0}};
+// 0 is the configured default (cost = -1, cframe = -1: waveCostHooks and the
+// environment as they are); the last one is the round-3 planner (no
+// compute-aware passes, no conditional frame)
+const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1}, {1, 1, 0, -1, 1}, {0, 0, 0, -1, 1}, {1, 0, 0, -1, 1},
+                                    {0, 2, 0, -1, 1},  {0, 1, 48, -1, 1}, {0, 1, 0, 0.5, 1}, {0, 0, 0, -1, 0}};
 constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
 
 void strategyHooks(const WaveStrategy& st, PlanHooks& h) {
     PlanHooks costed;
     waveCostHooks(costed);
     const double M = costed.memCost > 0 ? costed.memCost : 12800.0;
+    h.seeds = st.seeds;
+    h.lookahead = st.look;
+    if (st.cost < 0) {   // as configured
+        h.passCost = nullptr;
+        h.memCost = 0;
+        waveCostHooks(h);
+        return;
+    }
     h.passCost = nullptr;
     h.memCost = 0;
     if (st.cost) {
@@ -395,13 +404,17 @@ bool waveFrontSearch() {
 }
 
 int waveFrontStrategy() {
-    static const int v = getenv("QUEST_PLAN_FRONT_STRATEGY") ? atoi(getenv("QUEST_PLAN_FRONT_STRATEGY")) : 0;
+    static const int v = getenv("QUEST_PLAN_FRONT_STRATEGY") ? atoi(getenv("QUEST_PLAN_FRONT_STRATEGY")) : -1;
     return v;
 }
 
-int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const PlanHooks& base) {
+bool waveSearchOn() {
     static const bool on = !getenv("QUEST_PLAN_SEARCH") || atoi(getenv("QUEST_PLAN_SEARCH")) != 0;
-    if (!on || ops.size() < waveSearchMinOps() || L < kWaveBits + 6) return -1;
+    return on;
+}
+
+int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const PlanHooks& base) {
+    if (!waveSearchOn() || ops.size() < waveSearchMinOps() || L < kWaveBits + 6) return -1;
     PlanHooks costed;
     waveCostHooks(costed);
     const double M = costed.memCost > 0 ? costed.memCost : 12800.0;
@@ -442,7 +455,7 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
 
 WaveStrategyScope::WaveStrategyScope(int idx, int cdefault, PlanHooks& hooks, int* cmin) {
     *cmin = cdefault;
-    if (idx < 0 || idx >= kNumStrategies) return;
+    if (idx <= 0 || idx >= kNumStrategies) return;   // 0 / -1: as configured
     *cmin = cdefault + kStrategies[idx].dc;
     strategyHooks(kStrategies[idx], hooks);
     t_waveCframe = kStrategies[idx].cframe;

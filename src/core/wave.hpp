@@ -234,6 +234,7 @@ size_t waveSearchMinOps();
 // QUEST_PLAN_FRONT_STRATEGY: the strategy of front flushes until a search
 // has chosen one (default 0)
 bool waveFrontSearch();
+bool waveSearchOn();   // QUEST_PLAN_SEARCH (default 1)
 int waveFrontStrategy();
 // Plan (and lower) a flush with strategy idx (< 0: the default): sets the
 // hooks' knobs and *cmin, and the thread's conditional-frame switch until

@@ -472,7 +472,8 @@ void flushImpl(QuregImpl& q, bool front) {
     if (leftover.empty()) {   // the queue drained: choose afresh next time
         q.waveCmin = -1;
         q.planStrategy = -1;
-    } else if (front && searchable && waveFrontSearch() && q.planStrategy < 0 && !q.strategySearch.valid() &&
+    } else if (front && searchable && waveFrontSearch() && waveSearchOn() && q.planStrategy < 0 &&
+               !q.strategySearch.valid() &&
                leftover.size() >= waveSearchMinOps()) {
         PlanHooks base;
         base.relabelOk = hooks.relabelOk;
