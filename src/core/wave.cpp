@@ -322,6 +322,7 @@ double waveOpCycles(const WaveOp& w) {
         case WKind::DNEG: c = 61; break;
         case WKind::DMULI: case WKind::DMULNI: c = 236; break;
         case WKind::DROTN: c = 259; break;
+        case WKind::DSC: c = 128; break;
         default: c = 300; break;   // channels
     }
     const bool slotKind = w.kind != (int)WKind::TR && w.kind != (int)WKind::D2L &&
@@ -1405,6 +1406,11 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     }
     if (cframeOn) frameAfter();
     if (!sig.one()) settleScale(out, wp.opBegin, sig.re, sig.im);
+    // real diagonal factors (density dephasing) as DSC: two multiplies per
+    // amplitude instead of a complex product (QUEST_WAVE_DSC=0: keep DIAG)
+    static const bool dscOn = !getenv("QUEST_WAVE_DSC") || atoi(getenv("QUEST_WAVE_DSC")) != 0;
+    for (size_t o = (size_t)wp.opBegin; o < out.ops.size() && dscOn; o++)
+        if (out.ops[o].kind == (int)WKind::DIAG && out.ops[o].m[1] == 0) out.ops[o].kind = (int)WKind::DSC;
     if (endLanes)
         for (int l = 0; l < 3; l++) endLanes[l] = lay.laneBit[l];
     // store layout: the tile bits STORED to positions VB..VB+2 on lane bits

@@ -105,6 +105,9 @@ enum class WKind : int {
     // x1, x2 scaled by m[4] (CHD: the scaling only)
     CH1 = 23,
     CHD = 24,
+    // real factor m[0] on the (cReg, cLane) registers (PH_KINDS "DSC"): the
+    // real diagonal factors of density dephasing, half a complex product
+    DSC = 25,
 };
 
 // Whether a Mat4 (4x4, row-major, interleaved re/im as in TileOp::m) is a

@@ -106,6 +106,14 @@ void applyWaveOp(const WaveOp& w, real (*vr)[kWaveRegs], real (*vi)[kWaveRegs]) 
             }
             continue;
         }
+        if (kind == WKind::DSC) {
+            for (int j = 0; j < kWaveRegs; j++) {
+                if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
+                r[j] *= m[0];
+                i[j] *= m[0];
+            }
+            continue;
+        }
         if (kind >= WKind::DROT && kind <= WKind::DROTN) {
             for (int j = 0; j < kWaveRegs; j++) {
                 if ((((unsigned)j ^ w.fReg) & w.cReg) != w.cReg) continue;
@@ -225,7 +233,7 @@ void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
     }
     static const char* kName[] = {"M2", "M2R", "M2RI", "ANTI", "SWAP", "DIAG", "D2S", "D2L", "TR", "LM2R", "LM2RI",
                                   "LANTI", "LSWAP", "ROTY", "ROTX", "HADD", "YSW", "YSWC", "DROT", "DNEG", "DMULI",
-                                  "DMULNI", "DROTN", "CH1", "CHD"};
+                                  "DMULNI", "DROTN", "CH1", "CHD", "DSC"};
     for (int i = ps.opBegin; i < ps.opEnd && perOp; i++) {
         const WaveOp& w = wp.ops[(size_t)i];
         const unsigned lanes = w.cLane & 63u;
@@ -237,7 +245,7 @@ void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
                 else fprintf(stderr, "H wh_TRW_s%d_b%d\n", w.a, w.b - kWaveLanes);
                 break;
             case WKind::DIAG: case WKind::DROT: case WKind::DNEG: case WKind::DMULI: case WKind::DMULNI:
-            case WKind::DROTN:
+            case WKind::DROTN: case WKind::DSC:
                 fprintf(stderr, "H wh_%s_m%u_l%d\n", k, w.cReg, lanes ? 1 : 0);
                 break;
             case WKind::D2L: fprintf(stderr, "H wh_D2L_c%d\n", ctrl ? 1 : 0); break;

@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cstring>
 
+#include <type_traits>
+
 #include "qa_hip.h"
 
 namespace qa {
@@ -288,35 +290,42 @@ void launchCopyVec(void* dst, const void* src, size_t bytes, hipStream_t st) {
 }
 
 // a = alpha a + beta b, b in another qubit layout (PermArgs): per tile, b's
-// runs into LDS in a's element order, then a streamed in place
+// runs into LDS in a's element order (as innerPermKernel), then a streamed in
+// place, two elements per access
 template <typename T>
 __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, T* __restrict__ ai, T alpha,
                                                             const T* __restrict__ br, const T* __restrict__ bi,
                                                             T beta, PermArgs pa) {
+    using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
     extern __shared__ unsigned char smem[];
     T* sr = reinterpret_cast<T*>(smem);
     T* si = sr + (1 << pa.K);
-    const int E = 1 << pa.K;
+    PermLanes pl;
+    permLanes(pa, pl);
     const long long tiles = 1ll << pa.nOut;
     for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
         const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
         const unsigned long long baseB = scatterBits((unsigned long long)t, pa.oB, pa.nOut);
-        for (int f = threadIdx.x; f < E; f += kThreads) {
-            unsigned long long ob = 0;
-            int e = 0;
-            for (int m = 0; m < pa.K; m++)
-                if ((f >> m) & 1) {
-                    ob |= 1ull << pa.tB[pa.bOrd[m]];
-                    e |= 1 << pa.bOrd[m];
-                }
-            sr[e] = br[baseB | ob];
-            si[e] = bi[baseB | ob];
+        for (int q = 0; q < pl.n; q++) {
+            const V2 u = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
+            const V2 v = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
+            sr[pl.slotB0[q]] = u.x;
+            sr[pl.slotB1[q]] = u.y;
+            si[pl.slotB0[q]] = v.x;
+            si[pl.slotB1[q]] = v.y;
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < E; e += kThreads) {
-            const unsigned long long oa = baseA | scatterBits((unsigned long long)e, pa.tA, pa.K);
-            ar[oa] = alpha * ar[oa] + beta * sr[e];
-            ai[oa] = alpha * ai[oa] + beta * si[e];
+        for (int q = 0; q < pl.n; q++) {
+            V2* xr = reinterpret_cast<V2*>(ar + (baseA | pl.offA[q]));
+            V2* xi = reinterpret_cast<V2*>(ai + (baseA | pl.offA[q]));
+            const int s0 = pl.slotA[q], s1 = s0 ^ 1;
+            V2 x = *xr, y = *xi;
+            x.x = alpha * x.x + beta * sr[s0];
+            x.y = alpha * x.y + beta * sr[s1];
+            y.x = alpha * y.x + beta * si[s0];
+            y.y = alpha * y.y + beta * si[s1];
+            *xr = x;
+            *xi = y;
         }
         __syncthreads();
     }

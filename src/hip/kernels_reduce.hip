@@ -12,6 +12,7 @@
 #include "qa_hip.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace qa {
 namespace hipk {
@@ -258,38 +259,41 @@ __global__ __launch_bounds__(kThreads) void innerKernel(const T* __restrict__ ar
     }
 }
 
+
 // sum conj(a_i) b_sigma(i) with b in another qubit layout (PermArgs): per
-// tile, b's 16-element runs into LDS in a's element order, then a streamed
+// tile, b's 16-element runs into LDS in a's element order (2-element vector
+// loads, swizzled slots), then a streamed the same way
 template <typename T>
 __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict__ ar, const T* __restrict__ ai,
                                                             const T* __restrict__ br, const T* __restrict__ bi,
                                                             PermArgs pa, double* __restrict__ part) {
+    using V2 = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
     extern __shared__ unsigned char smem[];
     T* sr = reinterpret_cast<T*>(smem);
     T* si = sr + (1 << pa.K);
-    const int E = 1 << pa.K;
+    PermLanes pl;
+    permLanes(pa, pl);
     const long long tiles = 1ll << pa.nOut;
     double accR = 0, accI = 0;
     for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
         const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
         const unsigned long long baseB = scatterBits((unsigned long long)t, pa.oB, pa.nOut);
-        for (int f = threadIdx.x; f < E; f += kThreads) {
-            unsigned long long ob = 0;
-            int e = 0;
-            for (int m = 0; m < pa.K; m++)
-                if ((f >> m) & 1) {
-                    ob |= 1ull << pa.tB[pa.bOrd[m]];
-                    e |= 1 << pa.bOrd[m];
-                }
-            sr[e] = br[baseB | ob];
-            si[e] = bi[baseB | ob];
+        for (int q = 0; q < pl.n; q++) {
+            const V2 u = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
+            const V2 v = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
+            sr[pl.slotB0[q]] = u.x;
+            sr[pl.slotB1[q]] = u.y;
+            si[pl.slotB0[q]] = v.x;
+            si[pl.slotB1[q]] = v.y;
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < E; e += kThreads) {
-            const unsigned long long oa = baseA | scatterBits((unsigned long long)e, pa.tA, pa.K);
-            const double x = ar[oa], y = ai[oa], u = sr[e], v = si[e];
-            accR += x * u + y * v;
-            accI += x * v - y * u;
+        for (int q = 0; q < pl.n; q++) {
+            const V2 x = *reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q]));
+            const V2 y = *reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q]));
+            const int s0 = pl.slotA[q], s1 = s0 ^ 1;  // element f + 1: bit 0 is never swizzled
+            const double u0 = sr[s0], v0 = si[s0], u1 = sr[s1], v1 = si[s1];
+            accR += (double)x.x * u0 + (double)y.x * v0 + (double)x.y * u1 + (double)y.y * v1;
+            accI += (double)x.x * v0 - (double)y.x * u0 + (double)x.y * v1 - (double)y.y * u1;
         }
         __syncthreads();
     }

@@ -106,6 +106,11 @@ __device__ __forceinline__ void streamStore(V* p, V v) {
     }
 }
 
+// LDS slot of tile element e in the permuted kernels: b's elements are written
+// in its own order, scattered over a's; the XOR fold spreads a wave's writes
+// over the banks (a's reads of consecutive elements stay conflict-free)
+__device__ __forceinline__ int permSlot(int e) { return e ^ ((e >> 5) & 31) ^ ((e >> 10) & 31); }
+
 // PermArgs helpers: the bits of x scattered to positions pos[0..n)
 __device__ __forceinline__ unsigned long long scatterBits(unsigned long long x, const signed char* pos, int n) {
     unsigned long long r = 0;
@@ -147,6 +152,38 @@ struct PermArgs {
     signed char oA[48], oB[48];  // other bit m: position in a / in b
 };
 PermArgs makePermArgs(int L, const int* sig);
+
+#ifdef __HIPCC__
+// Per-thread element pairs of a permuted tile (E = 2^K <= 2048 elements,
+// 256 threads): pair g = threadIdx.x + 256 q.  b side, in b's order: its
+// elements 2g, 2g+1 (b-position 0 inside the pair: one 2-element load),
+// their a-order slots; a side: a's elements 2g, 2g+1 (a-position 0).
+struct PermLanes {
+    int n;                          // pairs of this thread
+    unsigned long long offB[4], offA[4];
+    int slotB0[4], slotB1[4], slotA[4];
+};
+
+__device__ __forceinline__ void permLanes(const PermArgs& pa, PermLanes& pl) {
+    const int pairs = 1 << (pa.K - 1);
+    pl.n = 0;
+    for (int g = threadIdx.x; g < pairs && pl.n < 4; g += blockDim.x, pl.n++) {
+        const int f = 2 * g;
+        unsigned long long ob = 0;
+        int e = 0;
+        for (int m = 1; m < pa.K; m++)
+            if ((f >> m) & 1) {
+                ob |= 1ull << pa.tB[pa.bOrd[m]];
+                e |= 1 << pa.bOrd[m];
+            }
+        pl.offB[pl.n] = ob;
+        pl.slotB0[pl.n] = permSlot(e);
+        pl.slotB1[pl.n] = permSlot(e | (1 << pa.bOrd[0]));
+        pl.offA[pl.n] = scatterBits((unsigned long long)f, pa.tA, pa.K);
+        pl.slotA[pl.n] = permSlot(f);
+    }
+}
+#endif  // __HIPCC__
 
 // ---- launchers (defined in kernels_*.hip) ----------------------------------
 void launchTilePass(real* re, real* im, const TileArgs& a, const TileOp* dOps, const TilePhase* dPhases,

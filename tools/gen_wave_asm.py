@@ -60,7 +60,7 @@ KINDS2 = ["ROTY", "ROTX", "HADD", "YSW", "YSWC"]
 # unit-modulus phases on the registers j with (j & creg) == creg (lane = 1:
 # only on lanes whose cLane bits are set): rotation of (re, im) by three
 # shears, negation, multiplication by +-i, negation + rotation
-PH_KINDS = ["DROT", "DNEG", "DMULI", "DMULNI", "DROTN"]
+PH_KINDS = ["DROT", "DNEG", "DMULI", "DMULNI", "DROTN", "DSC"]   # DSC: real scale m[0] (dephasing factors)
 # one-qubit density-matrix channels: a real superoperator on the 4-group of
 # slots (a, b) = (row bit, column bit), g = bit a + 2 bit b: CH1 mixes
 # (x0, x3) by a real 2x2 (m0 m1 / m2 m3) and scales x1, x2 by m4 (dephasing,
@@ -667,8 +667,9 @@ class Gen:
         self.back()
 
     def gen_ph(self, kind, creg, lane):
-        """Unit-modulus phase on the registers j with (j & creg) == creg of
-        the lanes whose cLane (s70) bits are set (lane = 1; exec-masked)."""
+        """Unit-modulus phase (DSC: a real factor) on the registers j with
+        (j & creg) == creg of the lanes whose cLane (s70) bits are set (lane =
+        1; exec-masked)."""
         self.handler(idx_ph(kind, creg, lane), f"{kind}_m{creg}_l{lane}")
         e = self.e
         if lane:
@@ -689,6 +690,9 @@ class Gen:
                 self.swap_vals(x, y)
                 r = x if kind == "DMULI" else y
                 e(f"v_xor_b32_e32 v{self.hi(r)}, 0x80000000, v{self.hi(r)}")
+            elif kind == "DSC":   # real factor: two multiplies instead of a complex product
+                e(f"{self.op('mul')} {self.vp(x)}, {self.sm(0)}, {self.vp(x)}")
+                e(f"{self.op('mul')} {self.vp(y)}, {self.sm(0)}, {self.vp(y)}")
         self.end_region()
         if lane:
             e("s_mov_b64 exec, -1")
