@@ -2,6 +2,7 @@
 // All grid-stride, 256 threads, 16-byte vector accesses where the layout
 // allows; launched on the backend stream.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include <type_traits>
@@ -292,7 +293,7 @@ void launchCopyVec(void* dst, const void* src, size_t bytes, hipStream_t st) {
 // a = alpha a + beta b, b in another qubit layout (PermArgs): per tile, b's
 // runs into LDS in a's element order (as innerPermKernel), then a streamed in
 // place, two elements per access
-template <typename T>
+template <typename T, int NP>
 __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, T* __restrict__ ai, T alpha,
                                                             const T* __restrict__ br, const T* __restrict__ bi,
                                                             T beta, PermArgs pa) {
@@ -300,13 +301,14 @@ __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, 
     extern __shared__ unsigned char smem[];
     T* sr = reinterpret_cast<T*>(smem);
     T* si = sr + (1 << pa.K);
-    PermLanes pl;
-    permLanes(pa, pl);
+    const PermLanes<NP> pl(pa);
     const long long tiles = 1ll << pa.nOut;
     for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
         const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
         const unsigned long long baseB = scatterBits((unsigned long long)t, pa.oB, pa.nOut);
-        for (int q = 0; q < pl.n; q++) {
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (!pl.live[q]) continue;
             const V2 u = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
             const V2 v = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
             sr[pl.slotB0[q]] = u.x;
@@ -314,12 +316,21 @@ __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, 
             si[pl.slotB0[q]] = v.x;
             si[pl.slotB1[q]] = v.y;
         }
+        V2 xa[NP], ya[NP];
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (!pl.live[q]) continue;
+            xa[q] = *reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q]));
+            ya[q] = *reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q]));
+        }
         __syncthreads();
-        for (int q = 0; q < pl.n; q++) {
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (!pl.live[q]) continue;
             V2* xr = reinterpret_cast<V2*>(ar + (baseA | pl.offA[q]));
             V2* xi = reinterpret_cast<V2*>(ai + (baseA | pl.offA[q]));
             const int s0 = pl.slotA[q], s1 = s0 ^ 1;
-            V2 x = *xr, y = *xi;
+            V2 x = xa[q], y = ya[q];
             x.x = alpha * x.x + beta * sr[s0];
             x.y = alpha * x.y + beta * sr[s1];
             y.x = alpha * y.x + beta * si[s0];
@@ -341,17 +352,27 @@ void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi,
 PermArgs makePermArgs(int L, const int* sig) {
     PermArgs pa;
     std::memset(&pa, 0, sizeof pa);
-    // tile: a's positions 0-3, those b holds on 0-3, then the lowest others
+    // tile: a's positions 0-3 and those b holds on 0-3 (16-element runs on
+    // both sides), then alternately a's and b's next lowest positions, so that
+    // both streams read runs as long as the tile allows
     bool inTile[64] = {false};
     int inv[64];
     for (int p = 0; p < L; p++) inv[sig[p]] = p;
     const int c = std::min(L, 4);
     for (int p = 0; p < c; p++) inTile[p] = inTile[inv[p]] = true;
-    const int K = std::min(L, 10);
+    // tile bits: more pairs per thread keep more loads in flight, fewer
+    // workgroups fit the LDS (QUEST_PERM_TILE_BITS, 8..12, default 11)
+    static const int bits = [] {
+        const char* e = std::getenv("QUEST_PERM_TILE_BITS");
+        return e ? std::max(8, std::min(kPermMaxBits, std::atoi(e))) : 11;
+    }();
+    const int K = std::min(L, bits);
     int k = 0;
     for (int p = 0; p < L; p++) k += inTile[p];
-    for (int p = 0; p < L && k < K; p++)
+    for (int p = c; p < L && k < K; p++) {
         if (!inTile[p]) inTile[p] = true, k++;
+        if (k < K && !inTile[inv[p]]) inTile[inv[p]] = true, k++;
+    }
     pa.K = k;
     int n = 0, m = 0;
     for (int p = 0; p < L; p++) {
@@ -376,8 +397,20 @@ void launchAxpbyPerm(real* ar, real* ai, real alpha, const real* br, const real*
     const long long tiles = 1ll << pa.nOut;
     const int grid = (int)std::min<long long>(tiles, 8ll * numCUs());
     const size_t lds = 2 * sizeof(real) << pa.K;
-    hipLaunchKernelGGL(axpbyPermKernel<real>, dim3(grid), dim3(kThreads), lds, stream(), ar, ai, alpha, br, bi, beta,
-                       pa);
+    switch (permPairsFor(pa.K)) {
+#define QA_AXPBY_PERM(NP)                                                                                            \
+    case NP:                                                                                                         \
+        hipLaunchKernelGGL((axpbyPermKernel<real, NP>), dim3(grid), dim3(kThreads), lds, stream(), ar, ai, alpha, br, \
+                           bi, beta, pa);                                                                            \
+        break;
+        QA_AXPBY_PERM(1)
+        QA_AXPBY_PERM(2)
+        QA_AXPBY_PERM(4)
+        QA_AXPBY_PERM(8)
+#undef QA_AXPBY_PERM
+    default:
+        fatal("launchAxpbyPerm", "tile bits out of range", __FILE__, __LINE__);
+    }
     QA_HIP_CHECK(hipGetLastError());
 }
 

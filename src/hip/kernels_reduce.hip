@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kThreads) void innerKernel(const T* __restrict__ ar
 // sum conj(a_i) b_sigma(i) with b in another qubit layout (PermArgs): per
 // tile, b's 16-element runs into LDS in a's element order (2-element vector
 // loads, swizzled slots), then a streamed the same way
-template <typename T>
+template <typename T, int NP>
 __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict__ ar, const T* __restrict__ ai,
                                                             const T* __restrict__ br, const T* __restrict__ bi,
                                                             PermArgs pa, double* __restrict__ part) {
@@ -271,14 +271,15 @@ __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict_
     extern __shared__ unsigned char smem[];
     T* sr = reinterpret_cast<T*>(smem);
     T* si = sr + (1 << pa.K);
-    PermLanes pl;
-    permLanes(pa, pl);
+    const PermLanes<NP> pl(pa);
     const long long tiles = 1ll << pa.nOut;
     double accR = 0, accI = 0;
     for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
         const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
         const unsigned long long baseB = scatterBits((unsigned long long)t, pa.oB, pa.nOut);
-        for (int q = 0; q < pl.n; q++) {
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (!pl.live[q]) continue;
             const V2 u = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
             const V2 v = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
             sr[pl.slotB0[q]] = u.x;
@@ -286,10 +287,18 @@ __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict_
             si[pl.slotB0[q]] = v.x;
             si[pl.slotB1[q]] = v.y;
         }
+        V2 xa[NP], ya[NP];
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (!pl.live[q]) continue;
+            xa[q] = *reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q]));
+            ya[q] = *reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q]));
+        }
         __syncthreads();
-        for (int q = 0; q < pl.n; q++) {
-            const V2 x = *reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q]));
-            const V2 y = *reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q]));
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (!pl.live[q]) continue;
+            const V2 x = xa[q], y = ya[q];
             const int s0 = pl.slotA[q], s1 = s0 ^ 1;  // element f + 1: bit 0 is never swizzled
             const double u0 = sr[s0], v0 = si[s0], u1 = sr[s1], v1 = si[s1];
             accR += (double)x.x * u0 + (double)y.x * v0 + (double)x.y * u1 + (double)y.y * v1;
@@ -491,8 +500,20 @@ void reduceInnerPerm(const real* ar, const real* ai, const real* br, const real*
     const long long tiles = 1ll << pa.nOut;
     const int nb = (int)std::min<long long>(tiles, kMaxBlocks);
     const size_t lds = 2 * sizeof(real) << pa.K;
-    hipLaunchKernelGGL(innerPermKernel<real>, dim3(nb), dim3(kThreads), lds, stream(), ar, ai, br, bi, pa,
-                       g_partials);
+    switch (permPairsFor(pa.K)) {
+#define QA_INNER_PERM(NP)                                                                                            \
+    case NP:                                                                                                         \
+        hipLaunchKernelGGL((innerPermKernel<real, NP>), dim3(nb), dim3(kThreads), lds, stream(), ar, ai, br, bi, pa,  \
+                           g_partials);                                                                              \
+        break;
+        QA_INNER_PERM(1)
+        QA_INNER_PERM(2)
+        QA_INNER_PERM(4)
+        QA_INNER_PERM(8)
+#undef QA_INNER_PERM
+    default:
+        fatal("reduceInnerPerm", "tile bits out of range", __FILE__, __LINE__);
+    }
     QA_HIP_CHECK(hipGetLastError());
     finish(nb, 2, out);
 }

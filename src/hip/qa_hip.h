@@ -144,6 +144,8 @@ struct TileArgs {
 // kernels (innerPermKernel, axpbyPermKernel) take tiles of 2^K amplitudes
 // whose a-positions include 0-3 and every position b holds on 0-3, so both
 // sides load 16-element runs; b goes through LDS into a's order.
+// most tile bits of the permuted kernels (4096 elements: 8 pairs a thread)
+constexpr int kPermMaxBits = 12;
 struct PermArgs {
     int K;                    // tile bits
     int nOut;                 // the other bits (L - K)
@@ -154,35 +156,43 @@ struct PermArgs {
 PermArgs makePermArgs(int L, const int* sig);
 
 #ifdef __HIPCC__
-// Per-thread element pairs of a permuted tile (E = 2^K <= 2048 elements,
-// 256 threads): pair g = threadIdx.x + 256 q.  b side, in b's order: its
-// elements 2g, 2g+1 (b-position 0 inside the pair: one 2-element load),
-// their a-order slots; a side: a's elements 2g, 2g+1 (a-position 0).
+// Per-thread element pairs of a permuted tile (E = 2^K elements, 256
+// threads, NP = max(1, E / 512) pairs a thread, compile-time so that the
+// per-pair state stays in registers): pair g = threadIdx.x + 256 q.  b side, in
+// b's order: its elements 2g, 2g+1 (b-position 0 inside the pair: one
+// 2-element load) and their a-order LDS slots; a side: a's elements 2g, 2g+1
+// (a-position 0).  live: g < E / 2 (only tiles under 512 elements leave
+// threads idle).
+template <int NP>
 struct PermLanes {
-    int n;                          // pairs of this thread
-    unsigned long long offB[4], offA[4];
-    int slotB0[4], slotB1[4], slotA[4];
-};
+    unsigned long long offB[NP], offA[NP];
+    int slotB0[NP], slotB1[NP], slotA[NP];
+    bool live[NP];
 
-__device__ __forceinline__ void permLanes(const PermArgs& pa, PermLanes& pl) {
-    const int pairs = 1 << (pa.K - 1);
-    pl.n = 0;
-    for (int g = threadIdx.x; g < pairs && pl.n < 4; g += blockDim.x, pl.n++) {
-        const int f = 2 * g;
-        unsigned long long ob = 0;
-        int e = 0;
-        for (int m = 1; m < pa.K; m++)
-            if ((f >> m) & 1) {
-                ob |= 1ull << pa.tB[pa.bOrd[m]];
-                e |= 1 << pa.bOrd[m];
-            }
-        pl.offB[pl.n] = ob;
-        pl.slotB0[pl.n] = permSlot(e);
-        pl.slotB1[pl.n] = permSlot(e | (1 << pa.bOrd[0]));
-        pl.offA[pl.n] = scatterBits((unsigned long long)f, pa.tA, pa.K);
-        pl.slotA[pl.n] = permSlot(f);
+    __device__ __forceinline__ explicit PermLanes(const PermArgs& pa) {
+        const int pairs = 1 << (pa.K - 1);
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            const int g = threadIdx.x + 256 * q;
+            live[q] = g < pairs;
+            const int f = 2 * g;
+            unsigned long long ob = 0;
+            int e = 0;
+            for (int m = 1; m < pa.K; m++)
+                if ((f >> m) & 1) {
+                    ob |= 1ull << pa.tB[pa.bOrd[m]];
+                    e |= 1 << pa.bOrd[m];
+                }
+            offB[q] = ob;
+            slotB0[q] = permSlot(e);
+            slotB1[q] = permSlot(e | (1 << pa.bOrd[0]));
+            offA[q] = scatterBits((unsigned long long)f, pa.tA, pa.K);
+            slotA[q] = permSlot(f);
+        }
     }
-}
+};
+// pairs per thread of a tile of K bits
+constexpr int permPairsFor(int K) { return K <= 9 ? 1 : 1 << (K - 9); }
 #endif  // __HIPCC__
 
 // ---- launchers (defined in kernels_*.hip) ----------------------------------

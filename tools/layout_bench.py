@@ -40,7 +40,8 @@ def main():
     out = {"qubits": n, "moved_a": sum(1 for i, p in enumerate(la) if i != p),
            "moved_b": sum(1 for i, p in enumerate(lb) if i != p),
            "perm_kernels": os.environ.get("QUEST_PERM_KERNELS", "1"),
-           "relayout_passes": os.environ.get("QUEST_RELAYOUT_PASSES", "1")}
+           "relayout_passes": os.environ.get("QUEST_RELAYOUT_PASSES", "1"),
+           "perm_tile_bits": os.environ.get("QUEST_PERM_TILE_BITS", "11")}
     ts = []
     for _ in range(3):
         t0 = time.perf_counter()
@@ -48,6 +49,10 @@ def main():
         ts.append(time.perf_counter() - t0)
     out["inner_ms"] = [round(1e3 * t, 3) for t in ts]
     out["inner"] = [ip.real, ip.imag]
+    # same registers, same layout: the plain streaming inner product
+    t0 = time.perf_counter()
+    a.inner(a)
+    out["inner_same_layout_ms"] = round(1e3 * (time.perf_counter() - t0), 3)
     capi.resetQuESTStats()
     t0 = time.perf_counter()
     capi.canonicaliseQureg(b.q)
