@@ -55,6 +55,20 @@ void exchangeWait(int slot);
 // Whether the transport can send from any device memory (RCCL: the state
 // itself), not only from comm buffers (IPC exports them, sockets stage them).
 bool sendsFromState();
+// In-place part swaps through the peers' mapped device memory (the IPC
+// transport: ranks of one node whose memory is mutually mappable).  Instead of
+// pack -> send -> receive -> unpack, one rank of each pair runs a kernel that
+// reads both parts and writes them swapped (router multiSwap / restore).
+// QUEST_IPC_SWAP=0 turns it off (the buffered pipeline then runs).
+bool swapsInPlace();
+// Collective with the listed peers (each must list this rank, in the same
+// pairwise (peer ^ rank) order): once the device work every one of them has
+// queued so far is complete, peerPtr[i * nArr + a] is a device pointer to
+// peer i's arrays[a] (the same role on every rank).
+void mapPeerArrays(const int* peers, int n, void* const* arrays, int nArr, void** peerPtr);
+// The device work this rank queued on the peers' memory is complete; returns
+// once every listed peer has said the same.
+void peersDone(const int* peers, int n);
 // In-place sum of host doubles across ranks.
 void allreduceSum(double* vals, int n);
 // In-place logical AND of a host int across ranks.

@@ -1,5 +1,7 @@
 // comm:: for the host (CPU) build: the socket mesh of comm_socket.cpp on
 // host buffers (the state lives in host memory).
+#include <cstdio>
+#include <cstdlib>
 #include "comm.hpp"
 
 namespace qa {
@@ -25,6 +27,12 @@ void exchange(const Xfer* x, int n) {
 }
 void exchangeAsync(const Xfer* x, int n, int) { exchange(x, n); }
 bool sendsFromState() { return false; }
+bool swapsInPlace() { return false; }
+void mapPeerArrays(const int*, int, void* const*, int, void**) {
+    fprintf(stderr, "QuEST: in-place peer swaps need the device IPC transport\n");
+    exit(EXIT_FAILURE);
+}
+void peersDone(const int*, int) {}
 void exchangeWait(int) {}
 void allreduceSum(double* vals, int n) { sock::allreduceSum(vals, n); }
 int allreduceAnd(int v) {

@@ -221,6 +221,36 @@ void transfer(const comm::Xfer* x, int n, int slot, hipStream_t producer, hipStr
     QA_HIP_CHECK(hipEventRecord(g_copied[slot], stream));
 }
 
+void mapArrays(const int* peers, int n, void* const* arrays, int nArr, void** out, hipStream_t producer) {
+    complete(0);
+    complete(1);
+    QA_HIP_CHECK(hipEventRecord(g_packed[0], producer));
+    hipk::syncStream(g_packed[0]);
+    std::vector<Token> mine((size_t)nArr), theirs((size_t)nArr);
+    for (int a = 0; a < nArr; a++) {
+        const Exported& e = exportBuffer(arrays[a]);
+        memset(&mine[(size_t)a], 0, sizeof(Token));
+        mine[(size_t)a].generation = g_generation;
+        mine[(size_t)a].id = e.id;
+        mine[(size_t)a].handle = e.handle;
+        mine[(size_t)a].offset = (unsigned long long)(static_cast<const char*>(arrays[a]) - e.base);
+    }
+    for (int i = 0; i < n; i++) {
+        sock::sendrecv(peers[i], mine.data(), theirs.data(), sizeof(Token) * (size_t)nArr);
+        for (int a = 0; a < nArr; a++)
+            out[(size_t)i * nArr + a] = importBuffer(peers[i], theirs[(size_t)a]) + theirs[(size_t)a].offset;
+    }
+}
+
+void done(const int* peers, int n, hipStream_t producer) {
+    QA_HIP_CHECK(hipEventRecord(g_copied[0], producer));
+    hipk::syncStream(g_copied[0]);
+    for (int i = 0; i < n; i++) {
+        int a = 1, b = 0;
+        sock::sendrecv(peers[i], &a, &b, sizeof a);
+    }
+}
+
 void forget(const void* p) {
     const char* c = static_cast<const char*>(p);
     for (size_t i = 0; i < g_exported.size(); i++)

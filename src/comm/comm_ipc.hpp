@@ -46,6 +46,12 @@ void finalize();
 void transfer(const comm::Xfer* x, int n, int slot, hipStream_t producer, hipStream_t stream);
 // Step 4 for the exchange last issued with `slot` (no-op if none pending).
 void complete(int slot);
+// In-place swaps (comm::mapPeerArrays / peersDone): the host waits for
+// `producer`, then one token round per peer trades IPC handles of the listed
+// arrays (any device allocation, the state included); done() waits for
+// `producer` again and trades a completion token with each peer.
+void mapArrays(const int* peers, int n, void* const* arrays, int nArr, void** out, hipStream_t producer);
+void done(const int* peers, int n, hipStream_t producer);
 // A comm buffer is about to be freed: forget its handle (a later allocation
 // at the same address gets a new id, so peers re-open it).
 void forget(const void* p);

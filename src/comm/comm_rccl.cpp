@@ -363,6 +363,19 @@ void exchange(const Xfer* x, int n) {
 
 bool sendsFromState() { return g_mode == Mode::Rccl; }
 
+bool swapsInPlace() {
+    // mapped address ranges (QUEST_ALLOC_MODE=3) have no IPC handle
+    static const bool on = (!getenv("QUEST_IPC_SWAP") || atoi(getenv("QUEST_IPC_SWAP")) != 0) &&
+                           !(getenv("QUEST_ALLOC_MODE") && atoi(getenv("QUEST_ALLOC_MODE")) == 3);
+    return on && g_mode == Mode::Ipc;
+}
+
+void mapPeerArrays(const int* peers, int n, void* const* arrays, int nArr, void** peerPtr) {
+    ipc::mapArrays(peers, n, arrays, nArr, peerPtr, S());
+}
+
+void peersDone(const int* peers, int n) { ipc::done(peers, n, S()); }
+
 bool pipelined() {
     static const bool off = getenv("QUEST_EXCHANGE_PIPELINE") && atoi(getenv("QUEST_EXCHANGE_PIPELINE")) == 0;
     return !off && (g_mode == Mode::Rccl || g_mode == Mode::Ipc) && g_cstream;

@@ -88,6 +88,11 @@ double densFidelity(QuregImpl& rho, const real* psiRe, const real* psiIm, int n,
 // Gather / scatter the amplitudes whose local bits pos[0..k) equal the
 // matching bits of setMask (k <= 8), in increasing index order: items
 // [start, start+count) of that sub-sequence.
+// Swap this chunk's amplitudes whose bits pos[0..k) = myMask with the
+// peer's (arrays peerRe / peerIm, mapped into this process) whose bits =
+// peerMask, at equal packed index, `count` each (comm::swapsInPlace)
+void swapPartsWithPeer(QuregImpl& q, real* peerRe, real* peerIm, const int* pos, int k, u64 myMask, u64 peerMask,
+                       i64 count);
 void packBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, real* bufRe, real* bufIm);
 void unpackBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, const real* bufRe,
                 const real* bufIm);

@@ -155,7 +155,7 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     // two buffer sets: slice s is packed into set s & 1 and exchanged on the
     // communication stream while slice s - 1 is unpacked and s + 1 packed
     const int np = parts - 1;
-    ensureXBuf(2 * np, slice);
+    if (!comm::swapsInPlace()) ensureXBuf(2 * np, slice);
     std::vector<comm::Xfer> xs[2] = {std::vector<comm::Xfer>(np), std::vector<comm::Xfer>(np)};
     std::vector<u64> setMask(parts);
     for (int j = 0; j < parts; j++) {
@@ -164,54 +164,77 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
             if ((j >> m) & 1) msk |= 1ull << lpos[m];
         setMask[j] = msk;
     }
-    const i64 nSlices = (partSize + slice - 1) / slice;
-    // the swapped local bits are the top k local positions: part j of the
-    // chunk is one contiguous range (its first amplitude index is setMask[j]),
-    // sent straight from the state -- no pack, one HBM round trip of 7/8 of
-    // the chunk fewer (transports that send from any device memory; RCCL)
-    bool top = comm::sendsFromState();
-    for (int m = 0; m < k; m++) top = top && lpos[m] >= q.L - k;
-    static const bool directOn = !getenv("QUEST_SWAP_DIRECT") || atoi(getenv("QUEST_SWAP_DIRECT")) != 0;
-    const bool direct = top && directOn;
-    if (direct)
-        for (int b = 0; b < 2; b++) xs[b].resize((size_t)(2 * np));
-    auto unpack = [&](i64 s) {
-        const int b = (int)(s & 1);
-        const i64 off = s * slice, n = std::min(slice, partSize - off);
+    if (comm::swapsInPlace()) {
+        // IPC: one kernel per rank pair, run by the lower rank, swaps the two
+        // parts in place through the peer's mapped state (no buffers; every
+        // amplitude read and written once)
+        std::vector<int> peers((size_t)np);
         for (int d = 1; d < parts; d++) {
-            real* r = g_x.recv[(size_t)(b * np + d - 1)];
-            be::unpackBits(q, lpos, k, setMask[myG ^ d], off, n, r, r + n);
-        }
-    };
-    for (i64 s = 0; s < nSlices; s++) {
-        const int b = (int)(s & 1);
-        const i64 off = s * slice, n = std::min(slice, partSize - off);
-        for (int d = 1; d < parts; d++) {
-            // peers are paired by logical chunk (step d matches chunk c with
-            // c ^ D(d) on every rank), then mapped to the rank holding it
             int peerChunk = q.chunkId;
             for (int m = 0; m < k; m++)
                 if ((d >> m) & 1) peerChunk ^= 1 << (gpos[m] - q.L);
-            real* rb = g_x.recv[(size_t)(b * np + d - 1)];
-            if (direct) {
-                const i64 at = (i64)setMask[myG ^ d] + off;
-                xs[b][(size_t)(2 * (d - 1))] = {rankOf(q, peerChunk), q.re + at, rb, sizeof(real) * (size_t)n};
-                xs[b][(size_t)(2 * (d - 1) + 1)] = {rankOf(q, peerChunk), q.im + at, rb + n, sizeof(real) * (size_t)n};
-                continue;
+            peers[(size_t)(d - 1)] = rankOf(q, peerChunk);
+        }
+        std::vector<void*> pp((size_t)(2 * np));
+        void* arrays[2] = {q.re, q.im};
+        comm::mapPeerArrays(peers.data(), np, arrays, 2, pp.data());
+        for (int d = 1; d < parts; d++)
+            if (rt().rank < peers[(size_t)(d - 1)])
+                be::swapPartsWithPeer(q, static_cast<real*>(pp[(size_t)(2 * (d - 1))]),
+                                      static_cast<real*>(pp[(size_t)(2 * (d - 1) + 1)]), lpos, k, setMask[myG ^ d],
+                                      setMask[myG], partSize);
+        comm::peersDone(peers.data(), np);
+        stats().bytesExchanged += (long long)(sizeof(real) * 2 * partSize) * np;
+    } else {
+        const i64 nSlices = (partSize + slice - 1) / slice;
+        // the swapped local bits are the top k local positions: part j of the
+        // chunk is one contiguous range (its first amplitude index is setMask[j]),
+        // sent straight from the state -- no pack, one HBM round trip of 7/8 of
+        // the chunk fewer (transports that send from any device memory; RCCL)
+        bool top = comm::sendsFromState();
+        for (int m = 0; m < k; m++) top = top && lpos[m] >= q.L - k;
+        static const bool directOn = !getenv("QUEST_SWAP_DIRECT") || atoi(getenv("QUEST_SWAP_DIRECT")) != 0;
+        const bool direct = top && directOn;
+        if (direct)
+            for (int b = 0; b < 2; b++) xs[b].resize((size_t)(2 * np));
+        auto unpack = [&](i64 s) {
+            const int b = (int)(s & 1);
+            const i64 off = s * slice, n = std::min(slice, partSize - off);
+            for (int d = 1; d < parts; d++) {
+                real* r = g_x.recv[(size_t)(b * np + d - 1)];
+                be::unpackBits(q, lpos, k, setMask[myG ^ d], off, n, r, r + n);
             }
-            real* sb = g_x.send[(size_t)(b * np + d - 1)];
-            be::packBits(q, lpos, k, setMask[myG ^ d], off, n, sb, sb + n);
-            xs[b][(size_t)(d - 1)] = {rankOf(q, peerChunk), sb, rb, sizeof(real) * 2 * (size_t)n};
+        };
+        for (i64 s = 0; s < nSlices; s++) {
+            const int b = (int)(s & 1);
+            const i64 off = s * slice, n = std::min(slice, partSize - off);
+            for (int d = 1; d < parts; d++) {
+                // peers are paired by logical chunk (step d matches chunk c with
+                // c ^ D(d) on every rank), then mapped to the rank holding it
+                int peerChunk = q.chunkId;
+                for (int m = 0; m < k; m++)
+                    if ((d >> m) & 1) peerChunk ^= 1 << (gpos[m] - q.L);
+                real* rb = g_x.recv[(size_t)(b * np + d - 1)];
+                if (direct) {
+                    const i64 at = (i64)setMask[myG ^ d] + off;
+                    xs[b][(size_t)(2 * (d - 1))] = {rankOf(q, peerChunk), q.re + at, rb, sizeof(real) * (size_t)n};
+                    xs[b][(size_t)(2 * (d - 1) + 1)] = {rankOf(q, peerChunk), q.im + at, rb + n, sizeof(real) * (size_t)n};
+                    continue;
+                }
+                real* sb = g_x.send[(size_t)(b * np + d - 1)];
+                be::packBits(q, lpos, k, setMask[myG ^ d], off, n, sb, sb + n);
+                xs[b][(size_t)(d - 1)] = {rankOf(q, peerChunk), sb, rb, sizeof(real) * 2 * (size_t)n};
+            }
+            comm::exchangeAsync(xs[b].data(), (int)xs[b].size(), b);
+            if (s > 0) {
+                comm::exchangeWait(1 - b);
+                unpack(s - 1);
+            }
+            stats().bytesExchanged += (long long)(sizeof(real) * 2 * n) * np;
         }
-        comm::exchangeAsync(xs[b].data(), (int)xs[b].size(), b);
-        if (s > 0) {
-            comm::exchangeWait(1 - b);
-            unpack(s - 1);
-        }
-        stats().bytesExchanged += (long long)(sizeof(real) * 2 * n) * np;
+        comm::exchangeWait((int)((nSlices - 1) & 1));
+        unpack(nSlices - 1);
     }
-    comm::exchangeWait((int)((nSlices - 1) & 1));
-    unpack(nSlices - 1);
     char moved[128];
     int at = 0;
     moved[0] = 0;
@@ -307,6 +330,17 @@ void issueRankAnti(QuregImpl& q, const Op& lop) {
 // slice s is copied out and exchanged on the communication stream while
 // slice s - 1 is copied in.
 void swapWholeChunk(QuregImpl& q, int peer, i64 slice) {
+    if (comm::swapsInPlace()) {
+        std::vector<void*> pp(2);
+        void* arrays[2] = {q.re, q.im};
+        comm::mapPeerArrays(&peer, 1, arrays, 2, pp.data());
+        if (rt().rank < peer)
+            be::swapPartsWithPeer(q, static_cast<real*>(pp[0]), static_cast<real*>(pp[1]), nullptr, 0, 0, 0,
+                                  q.numAmpsPerChunk);
+        comm::peersDone(&peer, 1);
+        stats().bytesExchanged += (long long)(sizeof(real) * 2 * q.numAmpsPerChunk);
+        return;
+    }
     const i64 nSlices = (q.numAmpsPerChunk + slice - 1) / slice;
     comm::Xfer xs[2];
     for (i64 s = 0; s < nSlices; s++) {
@@ -358,7 +392,7 @@ void restoreChunks(QuregImpl& q) {
         }
     }
     const i64 slice = std::min<i64>(q.numAmpsPerChunk, std::max<i64>(rt().exchangeSliceBytes / (i64)(2 * sizeof(real)), 1));
-    ensureXBuf(2, slice);
+    if (!comm::swapsInPlace()) ensureXBuf(2, slice);
     for (const std::vector<int>& pairOf : rounds) {
         bool any = false;
         for (int r = 0; r < R; r++) any = any || pairOf[(size_t)r] != r;

@@ -766,6 +766,11 @@ int sortedPositions(const int* pos, int k, int* out) {
 }
 }  // namespace
 
+void swapPartsWithPeer(QuregImpl&, real*, real*, const int*, int, u64, u64, i64) {
+    fprintf(stderr, "QuEST: in-place peer swaps need the HIP build's IPC transport\n");
+    exit(EXIT_FAILURE);
+}
+
 void packBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, real* br, real* bi) {
     flush(q);
     int sp[8];

@@ -147,6 +147,36 @@ __global__ __launch_bounds__(kThreads) void packRunKernel(T* __restrict__ re, T*
     }
 }
 
+// In-place exchange of two parts through a peer's mapped memory (the IPC
+// transport's swaps): a's amplitude at packed index j (bits pos[] = pb.setMask)
+// trades places with b's at the same j (bits pos[] = bMask).  Each amplitude
+// is read once and written once; the buffered pipeline (pack, pull, unpack)
+// moves it three times.  VEC: 16-byte units when the lowest inserted bit is
+// above the vector width.
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kThreads) void swapPartsKernel(T* __restrict__ ar, T* __restrict__ ai,
+                                                            T* __restrict__ br, T* __restrict__ bi, PackBits pb,
+                                                            long long bMask, long long count) {
+    using V = typename std::conditional<VEC, typename Vec16<T>::type, T>::type;
+    constexpr int VN = VEC ? Vec16<T>::n : 1;
+    const long long units = count / VN;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
+        long long i = u * VN;
+        for (int m = 0; m < pb.k; m++) i = ins0(i, pb.pos[m]);
+        const long long ia = i | pb.setMask, ib = i | bMask;
+        V* pa = reinterpret_cast<V*>(ar + ia);
+        V* qa = reinterpret_cast<V*>(ai + ia);
+        V* pbv = reinterpret_cast<V*>(br + ib);
+        V* qb = reinterpret_cast<V*>(bi + ib);
+        const V x = *pa, y = *qa, z = *pbv, w = *qb;
+        *pa = z;
+        *qa = w;
+        *pbv = x;
+        *qb = y;
+    }
+}
+
 // Device-to-device copy of n 16-byte vectors (runs of 256 x 4 per workgroup,
 // plus a tail loop): the IPC transport's pull from a peer's mapped buffer on
 // the same GPU, instead of the runtime's blit (~1 TB/s under contention).
@@ -342,6 +372,23 @@ __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, 
     }
 }
 
+
+void launchSwapParts(real* ar, real* ai, real* br, real* bi, const int* pos, int k, u64 aMask, u64 bMask, i64 count) {
+    constexpr int VN = Vec16<real>::n;
+    PackBits pb;
+    pb.k = k;
+    for (int m = 0; m < 8; m++) pb.pos[m] = m < k ? pos[m] : 0;
+    std::sort(pb.pos, pb.pos + k);
+    pb.setMask = (long long)aMask;
+    const bool vec = (k == 0 || (1ll << pb.pos[0]) >= VN) && count % VN == 0;
+    if (vec)
+        hipLaunchKernelGGL((swapPartsKernel<real, true>), dim3(gridFor(count / VN)), dim3(kThreads), 0, stream(), ar,
+                           ai, br, bi, pb, (long long)bMask, count);
+    else
+        hipLaunchKernelGGL((swapPartsKernel<real, false>), dim3(gridFor(count)), dim3(kThreads), 0, stream(), ar, ai,
+                           br, bi, pb, (long long)bMask, count);
+    QA_HIP_CHECK(hipGetLastError());
+}
 
 void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n) {
     hipLaunchKernelGGL(axpbyKernel<real>, dim3(gridFor(n / Vec16<real>::n)), dim3(kThreads), 0, stream(), ar, ai,

@@ -298,20 +298,22 @@ def test_reference_golden_suite_on_gpu(genv):
 
 
 _DIST = ["random_ops_statevector", "random_ops_density", "measurement_and_collapse", "calculations", "qasm_log",
-         "rank_qubit_gates", "top_swap"]
+         "rank_qubit_gates", "top_swap", "restore_chunks"]
 
 
-@pytest.mark.parametrize("transport,ranks,slice_kb", [("ipc", 2, ""), ("ipc", 4, ""), ("ipc", 4, "1"),
+@pytest.mark.parametrize("transport,ranks,slice_kb", [("ipc", 2, ""), ("ipc", 4, ""), ("ipc-buffered", 4, "1"),
                                                       ("ipc-nopipe", 2, "1"), ("socket", 2, ""), ("rccl", 2, ""),
                                                       ("rccl", 4, "1")])
 @pytest.mark.parametrize("name", _DIST)
 def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, slice_kb):
     """The distributed router with the HIP kernels (pack/unpack, chunk
     predicates, reductions + allreduce) on ONE GPU shared by 2 / 4 ranks,
-    against the single-rank HIP run.  QUEST_COMM=ipc moves the slices
-    GPU-to-GPU-buffer through HIP IPC on the communication stream with the
-    RCCL transport's event protocol (pack / exchange / unpack overlapped,
-    double-buffered); ipc-nopipe runs every exchange on the compute stream
+    against the single-rank HIP run.  QUEST_COMM=ipc swaps parts in place
+    (one kernel per rank pair through the peer's mapped state);
+    ipc-buffered (QUEST_IPC_SWAP=0) moves the slices GPU-to-GPU-buffer
+    through HIP IPC on the communication stream with the RCCL transport's
+    event protocol (pack / exchange / unpack overlapped, double-buffered);
+    ipc-nopipe runs every buffered exchange on the compute stream
     (QUEST_EXCHANGE_PIPELINE=0); socket stages through the host; rccl runs
     the production RCCL calls (grouped send / recv on the communication
     stream, allreduce, broadcast) with N ranks on the one GPU
@@ -330,7 +332,9 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     extra = {"QUEST_BACKEND": "hip", "QUEST_COMM": transport.split("-")[0], "PYTHONPATH": os.path.dirname(here),
              "QUEST_COMM_TIMEOUT": "180"}
     if transport == "ipc-nopipe":
-        extra["QUEST_EXCHANGE_PIPELINE"] = "0"
+        extra.update(QUEST_EXCHANGE_PIPELINE="0", QUEST_IPC_SWAP="0")
+    if transport == "ipc-buffered":
+        extra["QUEST_IPC_SWAP"] = "0"
     if transport == "rccl":
         # a rank that hangs dumps its Python stack and exits (QUEST_TEST_STACKS)
         extra.update(QUEST_RCCL_SHARED_GPU="1", QUEST_COMM_TIMEOUT="60", QUEST_TEST_STACKS="120")
@@ -346,10 +350,16 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
     assert int(got["_ranks"]) == ranks
     assert {"ipc": "IPC", "socket": "socket", "rccl": "RCCL"}[transport.split("-")[0]] in str(got["_transport"])
     for k, v in want.items():
+        if k.startswith("_"):
+            continue  # per-run statistics (swaps, restore rounds) depend on the rank count
         if isinstance(v, str):
             assert str(got[k]) == v, k
         else:
             np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+    if name == "restore_chunks":
+        # one concurrent round moving one chunk per rank (in place over IPC)
+        assert int(got["_xor_rounds"]) == 1
+        assert int(got["_xor_bytes"]) == 16 * (1 << (9 - {2: 1, 4: 2}[ranks]))
 
 
 def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):

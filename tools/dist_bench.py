@@ -74,6 +74,25 @@ def worker(args):
     for i in range(reps):
         reg.amp((i * 7919) % (1 << n))
     amp_ms = 1e3 * (time.perf_counter() - t1) / reps
+    # isolated swaps: a Hadamard on a qubit that sits on a rank position
+    # (every rank idle before and after), less a Hadamard on a local qubit
+    L = args.qubits
+    iso, local_h = [], []
+    for _ in range(3):
+        lay = qa.capi.getQubitLayout(reg.q)
+        qg = next(q for q in range(n) if lay[q] >= L)
+        ql = next(q for q in range(n) if lay[q] < L)
+        env.sync()
+        t1 = time.perf_counter()
+        reg.h(ql)
+        reg.sync()
+        env.sync()
+        local_h.append(1e3 * (time.perf_counter() - t1))
+        t1 = time.perf_counter()
+        reg.h(qg)
+        reg.sync()
+        env.sync()
+        iso.append(1e3 * (time.perf_counter() - t1))
     swap_ms = []
     tr = os.environ.get("QUEST_TRACE")
     if tr and os.path.exists(tr):
@@ -86,6 +105,7 @@ def worker(args):
            "gates": gates, "passes": st["passes"], "swaps": st["swaps"], "bytes_exchanged": st["bytesExchanged"],
            "relabels": st["relabels"], "swap_host_ms": swap_ms, "norm_error": abs(norm - 1),
            "total_prob_ms": scalar_ms, "get_amp_ms": amp_ms,
+           "isolated_swap_plus_h_ms": [round(x, 3) for x in iso], "local_h_ms": [round(x, 3) for x in local_h],
            "memory_plan_bytes": plan}
     out = args.out or os.environ.get("QUEST_DIST_BENCH_OUT")
     if out:
@@ -125,6 +145,7 @@ def launch(args):
                "swaps": ranks[0]["swaps"], "bytes_exchanged_per_rank": ranks[0]["bytes_exchanged"],
                "swap_host_ms_rank0": ranks[0]["swap_host_ms"], "norm_error": ranks[0]["norm_error"],
                "total_prob_ms": ranks[0]["total_prob_ms"], "get_amp_ms": ranks[0]["get_amp_ms"],
+               "isolated_swap_plus_h_ms": ranks[0]["isolated_swap_plus_h_ms"], "local_h_ms": ranks[0]["local_h_ms"],
                "memory_plan_bytes": ranks[0]["memory_plan_bytes"]}
     print(json.dumps(summary))
 
