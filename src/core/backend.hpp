@@ -90,9 +90,10 @@ double densFidelity(QuregImpl& rho, const real* psiRe, const real* psiIm, int n,
 // [start, start+count) of that sub-sequence.
 // Swap this chunk's amplitudes whose bits pos[0..k) = myMask with the
 // peer's (arrays peerRe / peerIm, mapped into this process) whose bits =
-// peerMask, at equal packed index, `count` each (comm::swapsInPlace)
+// peerMask, at equal packed index in [start, start + count)
+// (comm::swapsInPlace)
 void swapPartsWithPeer(QuregImpl& q, real* peerRe, real* peerIm, const int* pos, int k, u64 myMask, u64 peerMask,
-                       i64 count);
+                       i64 start, i64 count);
 void packBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, real* bufRe, real* bufIm);
 void unpackBits(QuregImpl& q, const int* pos, int k, u64 setMask, i64 start, i64 count, const real* bufRe,
                 const real* bufIm);

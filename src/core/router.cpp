@@ -165,9 +165,11 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         setMask[j] = msk;
     }
     if (comm::swapsInPlace()) {
-        // IPC: one kernel per rank pair, run by the lower rank, swaps the two
-        // parts in place through the peer's mapped state (no buffers; every
-        // amplitude read and written once)
+        // IPC: the two parts of each rank pair are swapped in place through
+        // the peer's mapped state (no buffers; every amplitude read and
+        // written once), each rank of the pair taking half of the range so
+        // that all ranks move the same bytes (between GPUs both directions of
+        // each link carry traffic)
         std::vector<int> peers((size_t)np);
         for (int d = 1; d < parts; d++) {
             int peerChunk = q.chunkId;
@@ -178,11 +180,13 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         std::vector<void*> pp((size_t)(2 * np));
         void* arrays[2] = {q.re, q.im};
         comm::mapPeerArrays(peers.data(), np, arrays, 2, pp.data());
-        for (int d = 1; d < parts; d++)
-            if (rt().rank < peers[(size_t)(d - 1)])
-                be::swapPartsWithPeer(q, static_cast<real*>(pp[(size_t)(2 * (d - 1))]),
-                                      static_cast<real*>(pp[(size_t)(2 * (d - 1) + 1)]), lpos, k, setMask[myG ^ d],
-                                      setMask[myG], partSize);
+        const i64 half = (partSize / 2) & ~(i64)15;
+        for (int d = 1; d < parts; d++) {
+            const bool low = rt().rank < peers[(size_t)(d - 1)];
+            be::swapPartsWithPeer(q, static_cast<real*>(pp[(size_t)(2 * (d - 1))]),
+                                  static_cast<real*>(pp[(size_t)(2 * (d - 1) + 1)]), lpos, k, setMask[myG ^ d],
+                                  setMask[myG], low ? 0 : half, low ? half : partSize - half);
+        }
         comm::peersDone(peers.data(), np);
         stats().bytesExchanged += (long long)(sizeof(real) * 2 * partSize) * np;
     } else {
@@ -334,9 +338,10 @@ void swapWholeChunk(QuregImpl& q, int peer, i64 slice) {
         std::vector<void*> pp(2);
         void* arrays[2] = {q.re, q.im};
         comm::mapPeerArrays(&peer, 1, arrays, 2, pp.data());
-        if (rt().rank < peer)
-            be::swapPartsWithPeer(q, static_cast<real*>(pp[0]), static_cast<real*>(pp[1]), nullptr, 0, 0, 0,
-                                  q.numAmpsPerChunk);
+        const i64 half = (q.numAmpsPerChunk / 2) & ~(i64)15;
+        const bool low = rt().rank < peer;
+        be::swapPartsWithPeer(q, static_cast<real*>(pp[0]), static_cast<real*>(pp[1]), nullptr, 0, 0, 0,
+                              low ? 0 : half, low ? half : q.numAmpsPerChunk - half);
         comm::peersDone(&peer, 1);
         stats().bytesExchanged += (long long)(sizeof(real) * 2 * q.numAmpsPerChunk);
         return;

@@ -632,6 +632,16 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         std::vector<int> kept;
         for (size_t x = 0; x < v.size(); x++)
             if (!drop[x]) kept.push_back(v[x]);
+        static const bool dbg = getenv("QUEST_PLAN_TRIM_DEBUG") != nullptr;
+        if (dbg) {
+            int movable = 0;
+            for (int i : v) {
+                const u64 tg = targetMask(ops[i]);
+                movable += ops[i].kind == OpKind::Diag || (ops[i].kind == OpKind::Mat2 && !(tg & ~low));
+            }
+            fprintf(stderr, "trim: C %.0f bound %.0f ops %zu movable %d dropped %zu\n", C, bound, v.size(), movable,
+                    v.size() - kept.size());
+        }
         if (kept.size() < v.size() && !kept.empty()) v.swap(kept);
     };
     while ((int)order.size() < n) {

@@ -766,7 +766,7 @@ int sortedPositions(const int* pos, int k, int* out) {
 }
 }  // namespace
 
-void swapPartsWithPeer(QuregImpl&, real*, real*, const int*, int, u64, u64, i64) {
+void swapPartsWithPeer(QuregImpl&, real*, real*, const int*, int, u64, u64, i64, i64) {
     fprintf(stderr, "QuEST: in-place peer swaps need the HIP build's IPC transport\n");
     exit(EXIT_FAILURE);
 }

@@ -156,13 +156,13 @@ __global__ __launch_bounds__(kThreads) void packRunKernel(T* __restrict__ re, T*
 template <typename T, bool VEC>
 __global__ __launch_bounds__(kThreads) void swapPartsKernel(T* __restrict__ ar, T* __restrict__ ai,
                                                             T* __restrict__ br, T* __restrict__ bi, PackBits pb,
-                                                            long long bMask, long long count) {
+                                                            long long bMask, long long start, long long count) {
     using V = typename std::conditional<VEC, typename Vec16<T>::type, T>::type;
     constexpr int VN = VEC ? Vec16<T>::n : 1;
     const long long units = count / VN;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
-        long long i = u * VN;
+        long long i = start + u * VN;
         for (int m = 0; m < pb.k; m++) i = ins0(i, pb.pos[m]);
         const long long ia = i | pb.setMask, ib = i | bMask;
         V* pa = reinterpret_cast<V*>(ar + ia);
@@ -373,20 +373,21 @@ __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, 
 }
 
 
-void launchSwapParts(real* ar, real* ai, real* br, real* bi, const int* pos, int k, u64 aMask, u64 bMask, i64 count) {
+void launchSwapParts(real* ar, real* ai, real* br, real* bi, const int* pos, int k, u64 aMask, u64 bMask, i64 start,
+                     i64 count) {
     constexpr int VN = Vec16<real>::n;
     PackBits pb;
     pb.k = k;
     for (int m = 0; m < 8; m++) pb.pos[m] = m < k ? pos[m] : 0;
     std::sort(pb.pos, pb.pos + k);
     pb.setMask = (long long)aMask;
-    const bool vec = (k == 0 || (1ll << pb.pos[0]) >= VN) && count % VN == 0;
+    const bool vec = (k == 0 || (1ll << pb.pos[0]) >= VN) && start % VN == 0 && count % VN == 0;
     if (vec)
         hipLaunchKernelGGL((swapPartsKernel<real, true>), dim3(gridFor(count / VN)), dim3(kThreads), 0, stream(), ar,
-                           ai, br, bi, pb, (long long)bMask, count);
+                           ai, br, bi, pb, (long long)bMask, start, count);
     else
         hipLaunchKernelGGL((swapPartsKernel<real, false>), dim3(gridFor(count)), dim3(kThreads), 0, stream(), ar, ai,
-                           br, bi, pb, (long long)bMask, count);
+                           br, bi, pb, (long long)bMask, start, count);
     QA_HIP_CHECK(hipGetLastError());
 }
 

@@ -211,8 +211,10 @@ void launchCopyVec(void* dst, const void* src, size_t bytes, hipStream_t st);
 void launchPackBits(const real* re, const real* im, const int* pos, int k, u64 setMask, i64 start, i64 count,
                     real* br, real* bi, bool unpack);
 // swap a's amplitudes with bits pos[0..k) = aMask and b's with bits = bMask,
-// at equal packed index (count per side; b may be a peer's mapped memory)
-void launchSwapParts(real* ar, real* ai, real* br, real* bi, const int* pos, int k, u64 aMask, u64 bMask, i64 count);
+// at equal packed index in [start, start + count) (b may be a peer's mapped
+// memory)
+void launchSwapParts(real* ar, real* ai, real* br, real* bi, const int* pos, int k, u64 aMask, u64 bMask, i64 start,
+                     i64 count);
 void launchAxpby(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, i64 n);
 // a = alpha a + beta b with b's amplitude sigma(i) for a's i (PermArgs)
 void launchAxpbyPerm(real* ar, real* ai, real alpha, const real* br, const real* bi, real beta, const PermArgs& pa);

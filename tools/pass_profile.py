@@ -58,10 +58,11 @@ def join(args):
         n = p["qubits"]
         tb = 2 * 16 * (1 << n) / 1e12   # fp64 re+im read and write, TB
         hi = [x for x in p["pos"] if x > 12]
-        out.append((ms, p["engine"], p["ops"], p.get("wave_ops", 0), p.get("wave_tr", 0), hi, tb / (ms / 1e3)))
-    print(f"{'ms':>7} {'engine':>6} {'ops':>4} {'wops':>5} {'tr':>4} {'TB/s':>5}  positions > 12")
-    for ms, eng, ops, wops, tr, hi, bw in out:
-        print(f"{ms:7.3f} {eng:>6} {ops:4d} {wops:5d} {tr:4d} {bw:5.2f}  {hi}")
+        out.append((ms, p["engine"], p["ops"], p.get("wave_ops", 0), p.get("wave_tr", 0), p.get("wave_cycles", 0), hi,
+                    tb / (ms / 1e3)))
+    print(f"{'ms':>7} {'engine':>6} {'ops':>4} {'wops':>5} {'tr':>4} {'cyc':>6} {'TB/s':>5}  positions > 12")
+    for ms, eng, ops, wops, tr, cyc, hi, bw in out:
+        print(f"{ms:7.3f} {eng:>6} {ops:4d} {wops:5d} {tr:4d} {cyc:6.0f} {bw:5.2f}  {hi}")
     tot = sum(o[0] for o in out)
     print(f"total {tot:.2f} ms over {len(out)} passes, mean {tot / max(1, len(out)):.3f} ms")
 

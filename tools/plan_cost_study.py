@@ -4,7 +4,9 @@
 circuit seed the pass count, the modeled compute of every pass (waveOpCycles
 summed over the pass's wave ops, the planner's own cost model) and
 sum(max(C, M)) with M = one pass's memory stream in the same units
-(QUEST_PLAN_MEM_CYCLES' default, 12800: about 5.6 ms at 30 qubits).
+(--score-mem, default 18000: the round-4 overlap study measured 3.6 ms of
+compute per 10^4 modeled cycles and 6.7 ms per memory-only pass at 30
+qubits, profiles/r4/overlap_study_r4b.txt).
 
     python tools/plan_cost_study.py [--seeds 7,1,2,3,4] [--set "name:ENV=V,ENV=V" ...]
 """
@@ -15,7 +17,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-M = 12800.0
+M = 18000.0
 
 
 def run(seed, env_over, qubits, layers):
@@ -36,11 +38,13 @@ def main():
     ap.add_argument("--seeds", default="7,1,2,3,4")
     ap.add_argument("--qubits", type=int, default=30)
     ap.add_argument("--layers", type=int, default=20)
+    ap.add_argument("--score-mem", type=float, default=M, help="M of the score, in modeled cycles")
     ap.add_argument("--set", action="append", default=[],
                     help='"name:ENV=V,ENV=V" (default: the build default and the planner without cost hooks)')
     args = ap.parse_args()
+    m = args.score_mem
     sets = args.set or ["default:", "nocost:QUEST_PLAN_MEM_CYCLES=0"]
-    print(f"# {args.qubits} qubits, {args.layers} layers; M = {M:.0f} modeled cycles per pass")
+    print(f"# {args.qubits} qubits, {args.layers} layers; M = {m:.0f} modeled cycles per pass")
     print(f"{'setting':24s} {'seed':>4s} {'passes':>6s} {'sumC':>8s} {'sumMax':>8s} {'maxC':>7s}")
     tot = {}
     for spec in sets:
@@ -48,7 +52,7 @@ def main():
         env = dict(x.split("=", 1) for x in kv.split(",") if x)
         for seed in args.seeds.split(","):
             P, cyc = run(int(seed), env, args.qubits, args.layers)
-            sm = sum(max(c, M) for c in cyc)
+            sm = sum(max(c, m) for c in cyc)
             t = tot.setdefault(name, [0, 0.0])
             t[0] += P
             t[1] += sm
