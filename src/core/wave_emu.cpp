@@ -271,6 +271,17 @@ void dumpWavePass(const WaveProgram& wp, const WavePass& ps) {
             ps.opEnd - ps.opBegin, cnt[0], cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], cnt[6], cnt[7], cnt[8], trw,
             cnt[9] + cnt[10] + cnt[11] + cnt[12], ctl, cnt[13], cnt[14], cnt[15], cnt[16] + cnt[17],
             cnt[18] + cnt[19] + cnt[20] + cnt[21] + cnt[22], cnt[23] + cnt[24], cyc);
+    // memory pattern: physical positions of the lane bits (one load / store
+    // instruction spans the vector bit and the real lane bits) and the slots
+    fprintf(stderr, "wave: ld lanes");
+    for (int l = 0; l < kWaveLaneBits; l++) fprintf(stderr, " %d", ps.pos[ps.ldLane[l]]);
+    fprintf(stderr, " slots");
+    for (int r = 0; r < kWaveSlots; r++) fprintf(stderr, " %d", ps.pos[ps.ldSlot[r]]);
+    fprintf(stderr, " | st lanes");
+    for (int l = 0; l < kWaveLaneBits; l++) fprintf(stderr, " %d", ps.stPos[ps.stLane[l]]);
+    fprintf(stderr, " slots");
+    for (int r = 0; r < kWaveSlots; r++) fprintf(stderr, " %d", ps.stPos[ps.stSlot[r]]);
+    fprintf(stderr, "\n");
     int trb[16] = {0};
     for (int i = ps.opBegin; i < ps.opEnd; i++)
         if (wp.ops[(size_t)i].kind == (int)WKind::TR) trb[wp.ops[(size_t)i].b & 15]++;

@@ -30,6 +30,12 @@ def main():
     reg = qa.Register(env, n)
     reg.init_plus()
     sets = {
+        # tile sets of the round-4 bench passes (profiles/r4/overlap_study_r4b.txt; slowest and fastest)
+        "r4 p0 0-7,9-13": [0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12, 13],
+        "r4 p1 14,15,21-23,25": [0, 1, 2, 3, 4, 5, 6, 14, 15, 21, 22, 23, 25],
+        "r4 p9 13,14,23-26": [0, 1, 2, 3, 4, 5, 6, 13, 14, 23, 24, 25, 26],
+        "r4 p7 7,8,10,18-20": [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 18, 19, 20],
+        "r4 p18 7,10,13,19,22,24": [0, 1, 2, 3, 4, 5, 6, 7, 10, 13, 19, 22, 24],
         "contiguous 0-12": list(range(13)),
         "0-3 + 4-12 (same)": list(range(13)),
         "0-3 + every 3rd": [0, 1, 2, 3, 7, 10, 13, 16, 19, 22, 25, 27, 29],
