@@ -12,6 +12,7 @@
 #include <vector>
 
 #include <omp.h>
+#include <sys/mman.h>
 
 #include "../core/backend.hpp"
 #include "../core/router.hpp"
@@ -349,9 +350,27 @@ std::string describe() { return "host C++ (plumbing build, no GPU)"; }
 const char* shortName() { return "CPU"; }
 bool stateOnHost() { return true; }
 
+namespace {
+// QUEST_PLAN_ONLY=1 (planner studies of registers larger than host memory):
+// the state is a lazily backed, unreserved mapping; pages no one touches
+// cost nothing
+bool planOnlyMode() {
+    static const bool on = getenv("QUEST_PLAN_ONLY") && atoi(getenv("QUEST_PLAN_ONLY")) != 0;
+    return on;
+}
+}  // namespace
+
 void allocState(QuregImpl& q) {
-    q.re = (real*)calloc((size_t)q.numAmpsPerChunk, sizeof(real));
-    q.im = (real*)calloc((size_t)q.numAmpsPerChunk, sizeof(real));
+    const size_t bytes = sizeof(real) * (size_t)q.numAmpsPerChunk;
+    if (planOnlyMode()) {
+        void* r = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        void* i = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        q.re = r == MAP_FAILED ? nullptr : static_cast<real*>(r);
+        q.im = i == MAP_FAILED ? nullptr : static_cast<real*>(i);
+    } else {
+        q.re = (real*)calloc((size_t)q.numAmpsPerChunk, sizeof(real));
+        q.im = (real*)calloc((size_t)q.numAmpsPerChunk, sizeof(real));
+    }
     if (!q.re || !q.im) {
         fprintf(stderr, "QuEST: could not allocate %lld amplitudes\n", q.numAmpsPerChunk);
         exit(EXIT_FAILURE);
@@ -359,8 +378,14 @@ void allocState(QuregImpl& q) {
 }
 
 void freeState(QuregImpl& q) {
-    free(q.re);
-    free(q.im);
+    if (planOnlyMode()) {
+        const size_t bytes = sizeof(real) * (size_t)q.numAmpsPerChunk;
+        munmap(q.re, bytes);
+        munmap(q.im, bytes);
+    } else {
+        free(q.re);
+        free(q.im);
+    }
     q.re = q.im = nullptr;
 }
 
@@ -539,6 +564,7 @@ void flushImpl(QuregImpl& q, bool front) {
 
 void fill(QuregImpl& q, real re, real im) {
     flush(q);
+    if (planOnlyMode()) return;   // the planner study never reads amplitudes
 #pragma omp parallel for if (q.numAmpsPerChunk >= kOmpMin)
     for (i64 i = 0; i < q.numAmpsPerChunk; i++) {
         q.re[i] = re;
