@@ -164,6 +164,7 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
             if ((j >> m) & 1) msk |= 1ull << lpos[m];
         setMask[j] = msk;
     }
+    bool direct = false;   // parts sent straight from the state
     if (comm::swapsInPlace()) {
         // IPC: the two parts of each rank pair are swapped in place through
         // the peer's mapped state (no buffers; every amplitude read and
@@ -198,7 +199,7 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         bool top = comm::sendsFromState();
         for (int m = 0; m < k; m++) top = top && lpos[m] >= q.L - k;
         static const bool directOn = !getenv("QUEST_SWAP_DIRECT") || atoi(getenv("QUEST_SWAP_DIRECT")) != 0;
-        const bool direct = top && directOn;
+        direct = top && directOn;
         if (direct)
             for (int b = 0; b < 2; b++) xs[b].resize((size_t)(2 * np));
         auto unpack = [&](i64 s) {
@@ -253,9 +254,15 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         q.p2l[l] = lg;
     }
     stats().swaps += k;
-    if (trace::on())
-        trace::event("swap", "\"k\": %d, \"bytes_sent\": %lld, \"host_ms\": %.3f, \"in_out\": [%s]", k,
-                     stats().bytesExchanged - bytes0, 1e3 * (trace::now() - t0), moved);
+    if (trace::on()) {
+        char lp[64];
+        int la = 0;
+        lp[0] = 0;
+        for (int m = 0; m < k && la < 56; m++) la += snprintf(lp + la, sizeof lp - (size_t)la, m ? ", %d" : "%d", lpos[m]);
+        trace::event("swap", "\"k\": %d, \"bytes_sent\": %lld, \"host_ms\": %.3f, \"in_out\": [%s], \"lpos\": [%s], "
+                     "\"direct\": %d", k, stats().bytesExchanged - bytes0, 1e3 * (trace::now() - t0), moved, lp,
+                     (int)direct);
+    }
 }
 
 u64 logicalTargets(const Op& op) {
@@ -450,6 +457,9 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
     std::sort(in.begin(), in.end(), [&](int a, int b) { return first[a] < first[b]; });
     for (int lg = 0; lg < q.nSV; lg++)
         if (q.l2p[lg] < q.L && !((need0 >> lg) & 1)) out.push_back(lg);
+    // (ties keep the logical order: breaking them by position -- to put
+    // victims on the top positions for direct sends -- moved which qubit the
+    // next window needs back and added a swap, host-build study)
     std::stable_sort(out.begin(), out.end(), [&](int a, int b) { return first[a] > first[b]; });
     int gp[8], lp[8], k = 0;
     for (size_t i = 0; i < in.size() && i < out.size() && k < 8; i++) {

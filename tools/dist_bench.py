@@ -93,17 +93,20 @@ def worker(args):
         reg.sync()
         env.sync()
         iso.append(1e3 * (time.perf_counter() - t1))
-    swap_ms = []
+    swap_ms, swap_lpos, swap_direct = [], [], []
     tr = os.environ.get("QUEST_TRACE")
     if tr and os.path.exists(tr):
         for line in open(tr):
             ev = json.loads(line)
             if ev.get("ev") == "swap":
                 swap_ms.append(ev.get("host_ms", 0.0))
+                swap_lpos.append([ev.get("lpos", []), ev.get("in_out", [])])
+                swap_direct.append(ev.get("direct", 0))
     res = {"rank": rank, "ranks": world, "qubits": n, "local_qubits": args.qubits,
            "transport": qa.capi.getQuESTTransport(), "s_per_gate": dt / max(gates, 1), "seconds": dt,
            "gates": gates, "passes": st["passes"], "swaps": st["swaps"], "bytes_exchanged": st["bytesExchanged"],
-           "relabels": st["relabels"], "swap_host_ms": swap_ms, "norm_error": abs(norm - 1),
+           "relabels": st["relabels"], "swap_host_ms": swap_ms, "swap_victim_positions": swap_lpos,
+           "swap_direct": swap_direct, "norm_error": abs(norm - 1),
            "total_prob_ms": scalar_ms, "get_amp_ms": amp_ms,
            "isolated_swap_plus_h_ms": [round(x, 3) for x in iso], "local_h_ms": [round(x, 3) for x in local_h],
            "memory_plan_bytes": plan}
@@ -143,7 +146,9 @@ def launch(args):
     summary = {"ranks": args.ranks, "qubits": worst["qubits"], "local_qubits": args.qubits,
                "transport": ranks[0]["transport"], "s_per_gate": worst["s_per_gate"], "passes": ranks[0]["passes"],
                "swaps": ranks[0]["swaps"], "bytes_exchanged_per_rank": ranks[0]["bytes_exchanged"],
-               "swap_host_ms_rank0": ranks[0]["swap_host_ms"], "norm_error": ranks[0]["norm_error"],
+               "swap_host_ms_rank0": ranks[0]["swap_host_ms"],
+               "swap_victim_positions": ranks[0]["swap_victim_positions"], "swap_direct": ranks[0]["swap_direct"],
+               "norm_error": ranks[0]["norm_error"],
                "total_prob_ms": ranks[0]["total_prob_ms"], "get_amp_ms": ranks[0]["get_amp_ms"],
                "isolated_swap_plus_h_ms": ranks[0]["isolated_swap_plus_h_ms"], "local_h_ms": ranks[0]["local_h_ms"],
                "memory_plan_bytes": ranks[0]["memory_plan_bytes"]}
