@@ -2,6 +2,7 @@
 (fp32/fp64 reference computations of the same ops), at qubit counts that
 exercise every tile geometry (whole-state tile, multi-tile, high targets,
 controls outside the tile) and the fused / unfused paths."""
+import json
 import math
 import os
 
@@ -360,6 +361,52 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
         # one concurrent round moving one chunk per rank (in place over IPC)
         assert int(got["_xor_rounds"]) == 1
         assert int(got["_xor_bytes"]) == 16 * (1 << (9 - {2: 1, 4: 2}[ranks]))
+
+
+IPC_F32 = r'''
+import json, os, sys
+import numpy as np
+import quest_amd as qa
+from quest_amd.models import random_layered
+from quest_amd.ops import capi
+env = qa.Env()
+n = 18
+r = qa.Register(env, n)
+r.init_plus()
+random_layered(n, 12, seed=5).apply(r)
+r.x(n - 1)                 # chunk relabel, then restored by the read
+r.ry(n - 2, 0.4)
+v = r.to_numpy()
+st = capi.getQuESTStats()
+if env.rank == 0:
+    np.save(sys.argv[1], v)
+    print("STATS " + json.dumps({"swaps": st["swaps"], "ranks": env.num_ranks, "transport": capi.getQuESTTransport()}))
+'''
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_ipc_in_place_swaps_fp32(genv, tmp_path, ranks):
+    """The fp32 library over the IPC transport: in-place part swaps
+    (swapPartsKernel on float vectors) and chunk restores against one rank."""
+    from quest_amd.parallel import spawn_local
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    one, dist = str(tmp_path / "one.npy"), str(tmp_path / "dist.npy")
+    base = {"QUEST_BACKEND": "hip", "QUEST_PREC": "1", "PYTHONPATH": os.path.dirname(here)}
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, "-c", IPC_F32, one], env=dict(os.environ, **base), capture_output=True,
+                       text=True, timeout=200)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    res = spawn_local(["-c", IPC_F32, dist], ranks, env_extra=dict(base, QUEST_COMM="ipc", QUEST_COMM_TIMEOUT="120"),
+                      timeout=200)
+    for r, q in enumerate(res):
+        assert q.returncode == 0, f"rank {r}:\n{q.stdout[-1500:]}\n{q.stderr[-2500:]}"
+    st = json.loads([ln for ln in res[0].stdout.splitlines() if ln.startswith("STATS")][0][6:])
+    assert st["ranks"] == ranks and "IPC" in st["transport"] and st["swaps"] >= 1, st
+    a, b = np.load(one), np.load(dist)
+    assert np.max(np.abs(a - b)) < 2e-6
 
 
 def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
