@@ -298,6 +298,13 @@ bool waveLowers(const TilePass& ps, const TileOp* ops) {
 // costs of profiles/r2/isa_micro_gfx950.txt); slot-controlled ops branch over
 // the registers that fail their controls.
 double waveOpCycles(const WaveOp& w) {
+    // round-4 calibration (tools/cost_fit.py: the per-pass compute of the
+    // --nomem kernel over 64 passes of three circuits against the handler
+    // mix): matrix handlers 1.5x, phases 1.25x, Ry / Rx 1.28x, register
+    // swaps 0.67x, lane swaps 0.75x, lane-0/1 transpositions 0.74x -- rms
+    // error per pass 0.27 -> 0.21 ms, same total (QUEST_WAVE_COST_MODEL=0:
+    // the round-3 table)
+    static const bool cal = !getenv("QUEST_WAVE_COST_MODEL") || atoi(getenv("QUEST_WAVE_COST_MODEL")) != 0;
     double c;
     switch ((WKind)w.kind) {
         case WKind::M2: c = 600; break;
@@ -324,6 +331,21 @@ double waveOpCycles(const WaveOp& w) {
         case WKind::DROTN: c = 259; break;
         case WKind::DSC: c = 128; break;
         default: c = 300; break;   // channels
+    }
+    if (cal) {
+        switch ((WKind)w.kind) {
+            case WKind::M2: case WKind::M2R: case WKind::M2RI: case WKind::ANTI: case WKind::D2S: case WKind::D2L:
+            case WKind::YSW: case WKind::YSWC: c *= 1.5; break;
+            case WKind::SWAP: c *= 0.67; break;
+            case WKind::LSWAP: c *= 0.75; break;
+            case WKind::TR: if (w.b < 2) c *= 0.74; else if (w.b >= kWaveLanes) c *= 0.88; break;
+            case WKind::ROTY: case WKind::ROTX: c *= 1.28; break;
+            case WKind::HADD: c *= 0.79; break;
+            case WKind::DNEG: c *= 1.31; break;
+            case WKind::DIAG: case WKind::DROT: case WKind::DMULI: case WKind::DMULNI: case WKind::DROTN:
+            case WKind::DSC: c *= 1.25; break;
+            default: break;
+        }
     }
     const bool slotKind = w.kind != (int)WKind::TR && w.kind != (int)WKind::D2L &&
                           (w.kind < (int)WKind::LM2R || w.kind > (int)WKind::LSWAP);

@@ -6,12 +6,12 @@
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 for v in full nomem noops; do
-  mkdir -p $R/gpurun_out/po/$v
+  mkdir -p $R/gpurun_out/po${SEED:-}/$v
   unset QUEST_LIB QUEST_WAVE_NOOPS
   [ $v = nomem ] && export QUEST_LIB=$R/quest_amd/lib/var/nomem.so
   [ $v = noops ] && export QUEST_WAVE_NOOPS=1
-  QUEST_TRACE=$R/gpurun_out/po/$v/trace.jsonl timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
-      -d $R/gpurun_out/po/$v -o run -- python3 $R/tools/pass_profile.py run --qubits ${QUBITS:-30} --layers ${LAYERS:-25} \
-      > $R/gpurun_out/po/$v/run.log 2>&1 || exit $?
-  python3 $R/tools/pass_profile.py join $R/gpurun_out/po/$v > $R/gpurun_out/po/$v/passes.txt 2>&1 || exit $?
+  QUEST_TRACE=$R/gpurun_out/po${SEED:-}/$v/trace.jsonl timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
+      -d $R/gpurun_out/po${SEED:-}/$v -o run -- python3 $R/tools/pass_profile.py run --qubits ${QUBITS:-30} --layers ${LAYERS:-25} --seed ${SEED:-7} \
+      > $R/gpurun_out/po${SEED:-}/$v/run.log 2>&1 || exit $?
+  python3 $R/tools/pass_profile.py join $R/gpurun_out/po${SEED:-}/$v > $R/gpurun_out/po${SEED:-}/$v/passes.txt 2>&1 || exit $?
 done
