@@ -114,6 +114,80 @@ struct Scale {  // complex factor the pass still owes its amplitudes
     bool one() const { return re == 1 && im == 0; }
 };
 
+bool isPhaseKind(int k) {
+    return k == (int)WKind::DNEG || k == (int)WKind::DMULI || k == (int)WKind::DMULNI || k == (int)WKind::DROT ||
+           k == (int)WKind::DROTN;
+}
+
+// The unit phase a phase op applies (phaseKind's inverse).
+void phaseOf(const WaveOp& w, double* pr, double* pi) {
+    switch ((WKind)w.kind) {
+        case WKind::DNEG: *pr = -1, *pi = 0; return;
+        case WKind::DMULI: *pr = 0, *pi = 1; return;
+        case WKind::DMULNI: *pr = 0, *pi = -1; return;
+        default: {
+            // rotParams: m[0] = tan(phi / 2), m[1] = sin(phi) of the phase with
+            // non-negative real part; DROTN negates it
+            const double t = w.m[0];
+            double c = (1 - t * t) / (1 + t * t), sn = w.m[1];
+            if (w.kind == (int)WKind::DROTN) c = -c, sn = -sn;
+            *pr = c;
+            *pi = sn;
+        }
+    }
+}
+
+// Merge the phase ops of every run of consecutive diagonal ops in
+// out.ops[begin..) that act on the same amplitudes (same register / lane /
+// wave / out-of-tile predicates): the product goes to the first of them,
+// identities disappear.
+void mergePhases(WaveProgram& out, size_t begin) {
+    std::vector<WaveOp>& ops = out.ops;
+    auto diag = [](int k) { return isPhaseKind(k) || k == (int)WKind::DIAG || k == (int)WKind::DSC; };
+    auto same = [](const WaveOp& x, const WaveOp& y) {
+        return x.a == y.a && x.b == y.b && x.cReg == y.cReg && x.cLane == y.cLane && x.cLaneZero == y.cLaneZero &&
+               x.fReg == y.fReg && x.fLane == y.fLane && x.ctrlOut == y.ctrlOut && x.ctrlOutZero == y.ctrlOutZero;
+    };
+    std::vector<char> gone(ops.size(), 0);
+    bool any = false;
+    size_t run = begin;
+    for (size_t k = begin; k <= ops.size(); k++) {
+        if (k < ops.size() && diag(ops[k].kind)) continue;
+        for (size_t x = run; x < k; x++) {
+            if (gone[x] || !isPhaseKind(ops[x].kind)) continue;
+            double pr, pi;
+            phaseOf(ops[x], &pr, &pi);
+            std::vector<size_t> ys;
+            for (size_t y = x + 1; y < k; y++) {
+                if (gone[y] || !isPhaseKind(ops[y].kind) || !same(ops[x], ops[y])) continue;
+                double qr, qi;
+                phaseOf(ops[y], &qr, &qi);
+                const double r = pr * qr - pi * qi, i = pr * qi + pi * qr;
+                pr = r, pi = i;
+                ys.push_back(y);
+            }
+            int kind;
+            real pm[2] = {0, 0};
+            if (ys.empty() || !phaseKind(pr, pi, &kind, pm)) continue;   // (products of unit phases stay unit)
+            for (size_t y : ys) gone[y] = 1;
+            any = true;
+            if (kind < 0) {
+                gone[x] = 1;
+                continue;
+            }
+            ops[x].kind = kind;
+            ops[x].m[0] = pm[0];
+            ops[x].m[1] = pm[1];
+        }
+        run = k + 1;
+    }
+    if (!any) return;
+    size_t w = begin;
+    for (size_t k = begin; k < ops.size(); k++)
+        if (!gone[k]) ops[w++] = ops[k];
+    ops.resize(w);
+}
+
 }  // namespace
 
 // Absorb the factor (sr, si) a pass owes its amplitudes: scale the matrix of
@@ -1433,6 +1507,12 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     static const bool dscOn = !getenv("QUEST_WAVE_DSC") || atoi(getenv("QUEST_WAVE_DSC")) != 0;
     for (size_t o = (size_t)wp.opBegin; o < out.ops.size() && dscOn; o++)
         if (out.ops[o].kind == (int)WKind::DIAG && out.ops[o].m[1] == 0) out.ops[o].kind = (int)WKind::DSC;
+    // phase ops on the same amplitudes inside a run of diagonal ops (they
+    // all commute) multiply into one, or vanish (Z Z, the CZ pairs the
+    // conditional frame puts around consecutive Ry / Rx on a conditioned
+    // target, T T -> S, ...): QUEST_WAVE_MERGE_PHASES=0 to keep them
+    static const bool mergeOn = !getenv("QUEST_WAVE_MERGE_PHASES") || atoi(getenv("QUEST_WAVE_MERGE_PHASES")) != 0;
+    if (mergeOn) mergePhases(out, (size_t)wp.opBegin);
     if (endLanes)
         for (int l = 0; l < 3; l++) endLanes[l] = lay.laneBit[l];
     // store layout: the tile bits STORED to positions VB..VB+2 on lane bits
