@@ -50,8 +50,9 @@ BASELINE_S_PER_OP = 3783.9266747315614 / 667  # fork's estimate, tutorial_exampl
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # default: the BASELINE's depth-30 circuit (30 timed layers, one layer a step)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--qubits", type=int, default=30, help="qubits per GPU")
     ap.add_argument("--eager", action="store_true", help="disable gate fusion (one pass per gate)")
     ap.add_argument("--seed", type=int, default=7)

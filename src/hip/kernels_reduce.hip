@@ -274,18 +274,28 @@ __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict_
     const PermLanes<NP> pl(pa);
     const long long tiles = 1ll << pa.nOut;
     double accR = 0, accI = 0;
-    for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
-        const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
-        const unsigned long long baseB = scatterBits((unsigned long long)t, pa.oB, pa.nOut);
+    // b's runs of the next tile are loaded while this one is reduced
+    // (software pipeline: one tile of b in registers ahead)
+    V2 ub[NP], vb[NP];
+    auto loadB = [&](long long tt) {
+        const unsigned long long baseB = scatterBits((unsigned long long)tt, pa.oB, pa.nOut);
 #pragma unroll
         for (int q = 0; q < NP; q++) {
             if (!pl.live[q]) continue;
-            const V2 u = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
-            const V2 v = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
-            sr[pl.slotB0[q]] = u.x;
-            sr[pl.slotB1[q]] = u.y;
-            si[pl.slotB0[q]] = v.x;
-            si[pl.slotB1[q]] = v.y;
+            ub[q] = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
+            vb[q] = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
+        }
+    };
+    if ((long long)blockIdx.x < tiles) loadB(blockIdx.x);
+    for (long long t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const unsigned long long baseA = scatterBits((unsigned long long)t, pa.oA, pa.nOut);
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            if (!pl.live[q]) continue;
+            sr[pl.slotB0[q]] = ub[q].x;
+            sr[pl.slotB1[q]] = ub[q].y;
+            si[pl.slotB0[q]] = vb[q].x;
+            si[pl.slotB1[q]] = vb[q].y;
         }
         V2 xa[NP], ya[NP];
 #pragma unroll
@@ -294,6 +304,7 @@ __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict_
             xa[q] = *reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q]));
             ya[q] = *reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q]));
         }
+        if (t + gridDim.x < tiles) loadB(t + gridDim.x);
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < NP; q++) {
