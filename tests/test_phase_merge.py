@@ -19,7 +19,8 @@ import quest_amd as qa
 from quest_amd.ops import capi
 from quest_amd.utils import oracle as O
 
-n = 16
+import sys
+n = int(sys.argv[1])
 e = qa.Env()
 r = qa.Register(e, n)
 rng = np.random.default_rng(11)
@@ -60,11 +61,11 @@ assert st["wavePasses"] >= 1, st
 '''
 
 
-def _run(backend, merge, tol):
+def _run(backend, merge, tol, n):
     env = dict(os.environ, QUEST_BACKEND=backend, QUEST_WAVE_MERGE_PHASES=merge)
     if backend == "cpu":
         env["QUEST_CPU_PLANNER"] = "3"
-    out = subprocess.run([sys.executable, "-c", SCRIPT.replace("TOL", repr(tol))], cwd=ROOT, env=env,
+    out = subprocess.run([sys.executable, "-c", SCRIPT.replace("TOL", repr(tol)), str(n)], cwd=ROOT, env=env,
                          capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("MERGE")][0]
@@ -72,17 +73,17 @@ def _run(backend, merge, tol):
     return int(f[4]), int(f[6])
 
 
-def _check(backend, tol):
-    ops_on, passes_on = _run(backend, "1", tol)
-    ops_off, passes_off = _run(backend, "0", tol)
+def _check(backend, tol, n):
+    ops_on, passes_on = _run(backend, "1", tol, n)
+    ops_off, passes_off = _run(backend, "0", tol, n)
     assert passes_on == passes_off   # the lowering, not the plan, changes
     assert ops_on < ops_off, (ops_on, ops_off)
 
 
 def test_phase_merge_on_the_wave_emulation():
-    _check("cpu", 1e-12)
+    _check("cpu", 1e-12, 16)
 
 
 @pytest.mark.gpu
 def test_phase_merge_gpu():
-    _check("hip", 1e-12)
+    _check("hip", 1e-12, 20)   # the GPU takes the wave engine from 19 local qubits
