@@ -410,10 +410,10 @@ void enqueue(QuregImpl& q, const Op& op) {
         return;
     }
     // front flushes of the wave planner, exactly as the HIP backend's
-    // (QUEST_FRONT_FLUSH, default 512 ops): the emulated plans stay the GPU's
+    // (QUEST_FRONT_FLUSH, default 600 ops): the emulated plans stay the GPU's
     static const size_t front = [] {
         const char* e = getenv("QUEST_FRONT_FLUSH");
-        return (size_t)std::max(0L, e ? atol(e) : 512L);
+        return (size_t)std::max(0L, e ? atol(e) : 600L);
     }();
     if (front && q.pending.size() >= front && ((q.pending.size() - front) & 15) == 0) flushImpl(q, true);
 }
