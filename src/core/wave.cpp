@@ -547,6 +547,12 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
     int best = 0;
     for (int i = 1; i < kNumStrategies; i++)
         if (score[i] < score[best] * (1 - 1e-9)) best = i;
+    static const bool dbg = getenv("QUEST_PLAN_SEARCH_DEBUG") != nullptr;
+    if (dbg) {
+        fprintf(stderr, "search over %zu ops:", ops.size());
+        for (int i = 0; i < kNumStrategies; i++) fprintf(stderr, " %.0f", score[i]);
+        fprintf(stderr, " -> %d\n", best);
+    }
     return best;
 }
 
