@@ -340,8 +340,8 @@ __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, 
 #pragma unroll
         for (int q = 0; q < NP; q++) {
             if (!pl.live[q]) continue;
-            ub[q] = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
-            vb[q] = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
+            ub[q] = streamLoad(reinterpret_cast<const V2*>(br + (baseB | pl.offB[q])));
+            vb[q] = streamLoad(reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q])));
         }
     };
     if ((long long)blockIdx.x < tiles) loadB(blockIdx.x);
@@ -359,8 +359,8 @@ __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, 
 #pragma unroll
         for (int q = 0; q < NP; q++) {
             if (!pl.live[q]) continue;
-            xa[q] = *reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q]));
-            ya[q] = *reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q]));
+            xa[q] = streamLoad(reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q])));
+            ya[q] = streamLoad(reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q])));
         }
         if (t + gridDim.x < tiles) loadB(t + gridDim.x);
         __syncthreads();
@@ -375,8 +375,8 @@ __global__ __launch_bounds__(kThreads) void axpbyPermKernel(T* __restrict__ ar, 
             x.y = alpha * x.y + beta * sr[s1];
             y.x = alpha * y.x + beta * si[s0];
             y.y = alpha * y.y + beta * si[s1];
-            *xr = x;
-            *xi = y;
+            streamStore(xr, x);
+            streamStore(xi, y);
         }
         __syncthreads();
     }

@@ -282,8 +282,8 @@ __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict_
 #pragma unroll
         for (int q = 0; q < NP; q++) {
             if (!pl.live[q]) continue;
-            ub[q] = *reinterpret_cast<const V2*>(br + (baseB | pl.offB[q]));
-            vb[q] = *reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q]));
+            ub[q] = streamLoad(reinterpret_cast<const V2*>(br + (baseB | pl.offB[q])));
+            vb[q] = streamLoad(reinterpret_cast<const V2*>(bi + (baseB | pl.offB[q])));
         }
     };
     if ((long long)blockIdx.x < tiles) loadB(blockIdx.x);
@@ -301,8 +301,8 @@ __global__ __launch_bounds__(kThreads) void innerPermKernel(const T* __restrict_
 #pragma unroll
         for (int q = 0; q < NP; q++) {
             if (!pl.live[q]) continue;
-            xa[q] = *reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q]));
-            ya[q] = *reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q]));
+            xa[q] = streamLoad(reinterpret_cast<const V2*>(ar + (baseA | pl.offA[q])));
+            ya[q] = streamLoad(reinterpret_cast<const V2*>(ai + (baseA | pl.offA[q])));
         }
         if (t + gridDim.x < tiles) loadB(t + gridDim.x);
         __syncthreads();

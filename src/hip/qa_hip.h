@@ -79,6 +79,11 @@ template <>
 struct NativeVec<float4> {
     using type = qa_nf4;
 };
+typedef float qa_nf2 __attribute__((ext_vector_type(2)));
+template <>
+struct NativeVec<float2> {
+    using type = qa_nf2;
+};
 
 // NT = false: plain accesses (the direct kernels on states that stay in the
 // 256 MB Infinity Cache between gates, hipk::stateCached)
