@@ -466,8 +466,19 @@ struct WaveStrategy {
 // environment as they are); the last one is the round-3 planner (no
 // compute-aware passes, no conditional frame)
 const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1}, {1, 1, 0, -1, 1}, {0, 0, 0, -1, 1}, {1, 0, 0, -1, 1},
-                                    {0, 2, 0, -1, 1},  {0, 1, 48, -1, 1}, {0, 1, 0, 0.5, 1}, {0, 0, 0, -1, 0}};
+                                    {0, 2, 0, -1, 1},  {0, 1, 48, -1, 1}, {0, 1, 0, 0.5, 1}, {0, 0, 0, -1, 0},
+                                    {-1, 1, 0, -1, 1}, {-1, 0, 0, -1, 1}};
 constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
+// strategies the search tries (QUEST_PLAN_STRATEGIES, default 8: the last two,
+// one fewer resident low position, are opt-in)
+int searchStrategies() {
+    static const int n = [] {
+        const char* e = getenv("QUEST_PLAN_STRATEGIES");
+        const int v = e ? atoi(e) : 8;
+        return v < 1 ? 1 : v > kNumStrategies ? kNumStrategies : v;
+    }();
+    return n;
+}
 
 void strategyHooks(const WaveStrategy& st, PlanHooks& h) {
     PlanHooks costed;
@@ -544,16 +555,17 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
         t_waveCframe = -1;
     };
     std::vector<std::thread> pool;
-    for (int i = 1; i < kNumStrategies; i++) pool.emplace_back(run, i);
+    const int nStrat = searchStrategies();
+    for (int i = 1; i < nStrat; i++) pool.emplace_back(run, i);
     run(0);
     for (std::thread& th : pool) th.join();
     int best = 0;
-    for (int i = 1; i < kNumStrategies; i++)
+    for (int i = 1; i < nStrat; i++)
         if (score[i] < score[best] * (1 - 1e-9)) best = i;
     static const bool dbg = getenv("QUEST_PLAN_SEARCH_DEBUG") != nullptr;
     if (dbg) {
         fprintf(stderr, "search over %zu ops:", ops.size());
-        for (int i = 0; i < kNumStrategies; i++) fprintf(stderr, " %.0f", score[i]);
+        for (int i = 0; i < nStrat; i++) fprintf(stderr, " %.0f", score[i]);
         fprintf(stderr, " -> %d\n", best);
     }
     return best;
