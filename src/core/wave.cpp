@@ -1,5 +1,7 @@
 #include "wave.hpp"
 
+#include <chrono>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -556,6 +558,7 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
     };
     std::vector<std::thread> pool;
     const int nStrat = searchStrategies();
+    const auto tSearch0 = std::chrono::steady_clock::now();
     for (int i = 1; i < nStrat; i++) pool.emplace_back(run, i);
     run(0);
     for (std::thread& th : pool) th.join();
@@ -564,7 +567,8 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
         if (score[i] < score[best] * (1 - 1e-9)) best = i;
     static const bool dbg = getenv("QUEST_PLAN_SEARCH_DEBUG") != nullptr;
     if (dbg) {
-        fprintf(stderr, "search over %zu ops:", ops.size());
+        fprintf(stderr, "search over %zu ops (%.1f ms):", ops.size(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tSearch0).count());
         for (int i = 0; i < nStrat; i++) fprintf(stderr, " %.0f", score[i]);
         fprintf(stderr, " -> %d\n", best);
     }
