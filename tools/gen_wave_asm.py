@@ -1355,6 +1355,9 @@ class Gen:
         """Load or store the NG 16-byte groups of re and im (per lane) of the
         register set at `regbase`, tile base in bytes in s[bpair:bpair+1]."""
         e = self.e
+        prio = getattr(self, "setprio", False) and not self.nomem
+        if prio:
+            e("s_setprio 2")   # issue this tile's memory ahead of the other waves' arithmetic
         # group byte offsets, 8 per s_load_dwordx16
         for half in range(0, NG, 8):
             n = min(8, NG - half)
@@ -1382,6 +1385,8 @@ class Gen:
                     e(f"buffer_load_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen{LD_POLICY}")
                 else:
                     e(f"buffer_store_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen{ST_POLICY}")
+        if prio:
+            e("s_setprio 0")
 
     def descriptor(self):
         nv = self.nvgpr
@@ -1484,6 +1489,8 @@ def main():
     ap.add_argument("--wbits", type=int, default=3, help="2^wbits waves share a tile")
     ap.add_argument("--debug", action="store_true", help="record addressing state per wave and stop (no state access)")
     ap.add_argument("--nomem", action="store_true", help="experiment: drop the state loads and stores")
+    ap.add_argument("--setprio", action="store_true",
+                    help="experiment: raise the wave priority while issuing a tile's loads / stores")
     ap.add_argument("--lean", type=int, default=0, help="1: 80-VGPR layout, half outboxes (3 workgroups per CU)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--obj")
@@ -1495,6 +1502,7 @@ def main():
         dbuf = args.dbuf if args.dbuf >= 0 else (args.slots <= 4 and args.wbits <= 2)
         set_layout(args.slots)
         g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug, args.nomem, bool(args.lean))
+        g.setprio = args.setprio
         g.kernel()
         with open(args.out, "w") as f:
             f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
