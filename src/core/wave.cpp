@@ -511,6 +511,15 @@ size_t waveSearchMinOps() {
     return v;
 }
 
+int waveSearchMinQubits() {
+    // below it a pass streams in well under a millisecond and the search's
+    // host time (several ms a window) costs more than the passes it saves:
+    // 20-24 local qubits ran 2-3x slower with it, 26 13 % slower, 28 7 %
+    // faster (profiles/r4/search_small_registers.txt)
+    static const int v = getenv("QUEST_PLAN_SEARCH_QUBITS") ? atoi(getenv("QUEST_PLAN_SEARCH_QUBITS")) : 27;
+    return v;
+}
+
 bool waveFrontSearch() {
     static const bool v = !getenv("QUEST_PLAN_SEARCH_FRONT") || atoi(getenv("QUEST_PLAN_SEARCH_FRONT")) != 0;
     return v;
@@ -527,7 +536,7 @@ bool waveSearchOn() {
 }
 
 int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const PlanHooks& base) {
-    if (!waveSearchOn() || ops.size() < waveSearchMinOps() || L < kWaveBits + 6) return -1;
+    if (!waveSearchOn() || ops.size() < waveSearchMinOps() || L < kWaveBits + 6 || L < waveSearchMinQubits()) return -1;
     PlanHooks costed;
     waveCostHooks(costed);
     const double M = costed.memCost > 0 ? costed.memCost : 12800.0;

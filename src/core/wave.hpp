@@ -233,6 +233,8 @@ void waveCostHooks(PlanHooks& hooks);
 // flushes and in the background after a window's first front flush.
 int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const PlanHooks& base);
 size_t waveSearchMinOps();
+// local qubits from which the strategy search runs (QUEST_PLAN_SEARCH_QUBITS, 27)
+int waveSearchMinQubits();
 // QUEST_PLAN_SEARCH_FRONT=0: no background search after front flushes;
 // QUEST_PLAN_FRONT_STRATEGY: the strategy of front flushes until a search
 // has chosen one (default 0)

@@ -499,7 +499,7 @@ void flushImpl(QuregImpl& q, bool front) {
         q.planStrategy = -1;
     } else if (front && searchable && waveFrontSearch() && waveSearchOn() && q.planStrategy < 0 &&
                !q.strategySearch.valid() &&
-               leftover.size() >= waveSearchMinOps()) {
+               leftover.size() >= waveSearchMinOps() && q.L >= waveSearchMinQubits()) {
         PlanHooks base;
         base.relabelOk = hooks.relabelOk;
         base.lowPerm = hooks.lowPerm;
