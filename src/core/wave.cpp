@@ -511,6 +511,14 @@ size_t waveSearchMinOps() {
     return v;
 }
 
+int waveCostMinQubits() {
+    // compute-aware trimming costs a wave lowering per candidate pass: at 20
+    // local qubits (passes of ~10 us) that host time outweighs what it saves
+    // (profiles/r4/search_small_registers.txt: 2.11 -> 1.79 us / gate without)
+    static const int v = getenv("QUEST_PLAN_COST_QUBITS") ? atoi(getenv("QUEST_PLAN_COST_QUBITS")) : 22;
+    return v;
+}
+
 int waveSearchMinQubits() {
     // below it a pass streams in well under a millisecond and the search's
     // host time (several ms a window) costs more than the passes it saves:

@@ -235,6 +235,8 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
 size_t waveSearchMinOps();
 // local qubits from which the strategy search runs (QUEST_PLAN_SEARCH_QUBITS, 27)
 int waveSearchMinQubits();
+// local qubits from which passes are planned compute-aware (QUEST_PLAN_COST_QUBITS, 22)
+int waveCostMinQubits();
 // QUEST_PLAN_SEARCH_FRONT=0: no background search after front flushes;
 // QUEST_PLAN_FRONT_STRATEGY: the strategy of front flushes until a search
 // has chosen one (default 0)

@@ -458,7 +458,7 @@ void flushImpl(QuregImpl& q, bool front) {
     hooks.lowPerm = [](const TilePass& ps, const TileOp* ops, int c, int* sigma) {
         return waveLowPerm(ps, ops, c, sigma);
     };
-    waveCostHooks(hooks);
+    if (q.L >= waveCostMinQubits()) waveCostHooks(hooks);
     std::vector<Op> leftover;
     if (front) {
         // as the HIP backend: plain wave queues of wave-sized registers only
