@@ -146,7 +146,8 @@ void init(int rank, int size) {
     sa.sin_port = 0;
     sa.sin_addr.s_addr = htonl(INADDR_ANY);
     if (bind(ls, (sockaddr*)&sa, sizeof sa) != 0) die("bind");
-    if (listen(ls, size) != 0) die("listen");
+    // room for every peer's connect plus retries (as the bootstrap listener)
+    if (listen(ls, size * 8 > SOMAXCONN ? size * 8 : SOMAXCONN) != 0) die("listen");
     socklen_t len = sizeof sa;
     getsockname(ls, (sockaddr*)&sa, &len);
 
