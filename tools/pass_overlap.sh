@@ -3,9 +3,10 @@
 # compute only (tools/gen_wave_asm.py --nomem library in quest_amd/lib/var/
 # nomem.so) and memory only (QUEST_WAVE_NOOPS=1) -- each joined with the pass
 # trace (tools/pass_profile.py); then tools/pass_overlap.py compares them.
+# VARIANTS="noops": only some of the three.
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-for v in full nomem noops; do
+for v in ${VARIANTS:-full nomem noops}; do
   mkdir -p $R/gpurun_out/po${SEED:-}/$v
   unset QUEST_LIB QUEST_WAVE_NOOPS
   [ $v = nomem ] && export QUEST_LIB=$R/quest_amd/lib/var/nomem.so
