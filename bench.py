@@ -5,14 +5,20 @@ state-vector; 1/2/4/8-GPU scaling").
 
 Workload (weak scaling): QUBITS_PER_GPU (default 30) qubits per GPU, so N
 GPUs simulate 30 + log2(N) qubits, one rank per GPU (torchrun), the state
-sharded over ranks and exchanged with RCCL over xGMI.  One *step* = one layer
-of a seeded random circuit: a random gate from {H, X, Y, Z, S, T, Rx, Ry, Rz}
-on every qubit, then a brick layer of CNOTs (the fork benchmark's gate mix,
-tutorial_example.c:29-518).  `value` = wall seconds per gate over the timed
-steps (max over ranks), gates applied through the public API exactly as a
-user would call them (hadamard(), rotateX(), controlledNot(), ...).
+sharded over ranks and exchanged with RCCL over xGMI.  The workload is a
+seeded random layered circuit: every layer is a random gate from {H, X, Y, Z,
+S, T, Rx, Ry, Rz} on every qubit, then a brick layer of CNOTs (the fork
+benchmark's gate mix, tutorial_example.c:29-518).  Five circuit seeds (7, and
+11, 12, 13, 17, which no tuning ever used) run in one register each, every
+one in its own window: K timed layers queued, then one sync, seed after seed.
+A *step* is one layer of every seed's circuit.  `value` = wall seconds per
+gate over all timed windows (the mean over the seeds; max over ranks), gates
+applied through the public API exactly as a user would call them
+(hadamard(), rotateX(), controlledNot(), ...).  `config.seeds` has each
+seed's s/gate, window time and pass count (and at N > 1 its swaps, bytes sent
+per rank, swap device time and the swap share of the window).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--qubits Q] [--eager] [--no-extras]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--qubits Q] [--seeds 7,11,...] [--eager] [--no-extras]
 
 Besides the headline, a single-GPU run adds (outside the timed region, ~10 s):
   * ``sweep``: the metric's "vs #qubits" axis -- unfused Hadamard on targets
@@ -20,7 +26,11 @@ Besides the headline, a single-GPU run adds (outside the timed region, ~10 s):
     streaming pass per gate), with the achieved HBM bandwidth;
   * ``fork30``: the fork's own 30-qubit program end to end (490 gates, 30
     calcProbOfOutcome, 10 getAmp; tutorial_example.c:1-3, 29-534);
-  * ``window1_s_per_gate``: the headline circuit flushed after every layer
+  * ``rotate29``: the reference's per-target benchmark
+    (tests/benchmarks/rotate_benchmark.test): compactUnitary on every target
+    of a 29-qubit register, 20 synced trials each, mean / stdev / min / max and
+    TB/s per target;
+  * ``window1_s_per_gate``: the seed-7 circuit flushed after every layer
     (the scheduler sees one layer at a time, as in a program that reads the
     state between layers);
   * ``q34``: 34 qubits (256 GiB, the largest state one MI355X holds): unfused
@@ -29,7 +39,7 @@ Besides the headline, a single-GPU run adds (outside the timed region, ~10 s):
     dephasing, two-qubit dephasing and depolarising per channel, gates;
   * ``fp32``: the headline circuit with the QUEST_PREC=1 library (a child
     process), its s/gate and the ratio to fp64.
-  (--extras q34,fp32 picks some; --no-extras none)
+  (--extras q34,fp32 picks some; --no-extras none; the extras use the first seed)
 A multi-GPU run must use RCCL (``--allow-transport`` accepts another one).
 """
 from __future__ import annotations
@@ -47,20 +57,34 @@ sys.path.insert(0, ROOT)
 BASELINE_S_PER_OP = 3783.9266747315614 / 667  # fork's estimate, tutorial_example.c:1-3
 
 
+DEFAULT_SEEDS = "7,11,12,13,17"   # 7: the rounds-1..4 headline; 11-13, 17 never used for tuning
+
+
+def split_layers(circ, n, layers):
+    """The circuit's gates per layer (n one-qubit gates + a CNOT brick)."""
+    out, i = [], 0
+    for layer in range(layers):
+        cnt = n + len(range(layer % 2, n - 1, 2))
+        out.append(circ.gates[i:i + cnt])
+        i += cnt
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    # default: the BASELINE's depth-30 circuit (30 timed layers, one layer a step)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20, help="timed layers of every seed's circuit")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed layers of every seed's circuit before")
     ap.add_argument("--qubits", type=int, default=30, help="qubits per GPU")
     ap.add_argument("--eager", action="store_true", help="disable gate fusion (one pass per gate)")
-    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--seeds", default=DEFAULT_SEEDS, help="comma-separated circuit seeds, one window each")
+    ap.add_argument("--seed", type=int, default=None, help="a single circuit seed (overrides --seeds)")
     ap.add_argument("--no-extras", action="store_true", help="skip every extra (single-GPU runs only)")
-    ap.add_argument("--extras", default="window1,fork30,sweep,q34,density17,fp32",
+    ap.add_argument("--extras", default="window1,fork30,sweep,rotate29,q34,density17,fp32",
                     help="comma-separated extras of a single-GPU run")
     ap.add_argument("--allow-transport", action="store_true", help="accept a non-RCCL transport with N > 1")
     args = ap.parse_args()
+    seeds = [args.seed] if args.seed is not None else [int(x) for x in args.seeds.split(",") if x]
 
     from quest_amd.parallel import allreduce_max, barrier, init_distributed
 
@@ -75,6 +99,7 @@ def main():
 
     import quest_amd as qa
     from quest_amd.models import random_layered
+    from quest_amd.models.circuits import Circuit
 
     if args.eager:
         os.environ["QUEST_FUSION"] = "0"
@@ -84,47 +109,63 @@ def main():
         print(f"bench.py: {world} ranks must exchange over RCCL, transport is '{transport}'", file=sys.stderr)
         sys.exit(3)
     n = args.qubits + int(round(math.log2(world)))
-    reg = qa.Register(env, n)
-    reg.init_plus()
-
     layers = args.warmup + args.steps
-    circ = random_layered(n, layers, seed=args.seed)
-    per_layer = len(circ.gates) // layers if layers else 0
-    # split into layers (each layer: n one-qubit gates + CNOT brick)
-    layer_gates = []
-    i = 0
-    for layer in range(layers):
-        cnt = n + len(range(layer % 2, n - 1, 2))
-        layer_gates.append(circ.gates[i:i + cnt])
-        i += cnt
-
-    from quest_amd.models.circuits import Circuit
-
-    def run_layer(idx):
-        Circuit(n, layer_gates[idx]).apply(reg)
-
-    for w in range(args.warmup):
-        run_layer(w)
-    reg.sync()
+    # one register per seed (16 GiB each at 30 qubits per GPU), every one
+    # warmed up with its own first W layers
+    regs, per_seed_layers = [], []
+    for sd in seeds:
+        r = qa.Register(env, n)
+        r.init_plus()
+        lg = split_layers(random_layered(n, layers, seed=sd), n, layers)
+        for w in range(args.warmup):
+            Circuit(n, lg[w]).apply(r)
+        r.sync()
+        regs.append(r)
+        per_seed_layers.append(lg)
     qa.capi.resetQuESTStats()
 
+    # timed: every seed's K layers in its own window (queued, then one sync),
+    # one seed after another; a step = one layer of every seed's circuit
     barrier()
-    reg.sync()
+    for r in regs:
+        r.sync()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     gates = 0
-    for s in range(args.steps):
-        run_layer(args.warmup + s)
-        gates += len(layer_gates[args.warmup + s])
-    reg.sync()
+    marks = []
+    for r, lg in zip(regs, per_seed_layers):
+        ts = time.perf_counter()
+        g = 0
+        for s in range(args.steps):
+            Circuit(n, lg[args.warmup + s]).apply(r)
+            g += len(lg[args.warmup + s])
+        r.sync()
+        st = qa.capi.getQuESTStats()
+        marks.append((time.perf_counter() - ts, g, st["passes"], st["swaps"], st["bytesExchanged"],
+                      st["swapMicros"]))
+        gates += g
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     barrier()
     elapsed = allreduce_max(time.perf_counter() - t0)
     stats = qa.capi.getQuESTStats()
+    seed_rows, prev = [], (0, 0, 0, 0)
+    for sd, (dt, g, p, sw, by, us) in zip(seeds, marks):
+        dt = allreduce_max(dt)
+        row = {"seed": sd, "s_per_gate": dt / max(g, 1), "window_ms": 1e3 * dt, "passes": p - prev[0]}
+        if world > 1:
+            swap_ms = allreduce_max((us - prev[3]) * 1e-3)
+            row.update({"swaps": sw - prev[1], "swap_bytes_per_rank": by - prev[2], "swap_ms": swap_ms,
+                        "swap_share": swap_ms / (1e3 * dt) if dt > 0 else None})
+        prev = (p, sw, by, us)
+        seed_rows.append(row)
 
+    reg = regs[0]
     norm = reg.total_prob()  # sanity (outside the timed region)
+    norm_err = max(abs(r.total_prob() - 1.0) for r in regs)
+    for r in regs[1:]:
+        r.close()
     # for reference, outside the timed region: one unfused gate (= one full
     # streaming pass over the state), median of 5
     qa.capi.setGateFusion(0)
@@ -141,13 +182,19 @@ def main():
     extras = {}
     if world == 1 and not args.no_extras and qa.capi.getQuESTBackend() == "HIP":
         try:
-            extras = run_extras(qa, reg, n, layer_gates, args)   # closes reg
+            extras = run_extras(qa, reg, n, per_seed_layers[0], args, seeds[0])   # closes reg
         except Exception as e:  # an optional extra must never cost the headline
             extras = {"extras_error": f"{type(e).__name__}: {e}"[:500]}
         if "s_per_gate" in extras.get("fp32", {}):
-            extras["fp32"]["ratio_to_fp64"] = extras["fp32"]["s_per_gate"] / (elapsed / max(gates, 1))
+            extras["fp32"]["ratio_to_fp64"] = extras["fp32"]["s_per_gate"] / seed_rows[0]["s_per_gate"]
     else:
         reg.close()
+    multi = {}
+    if world > 1:
+        swap_ms = sum(r["swap_ms"] for r in seed_rows)
+        multi = {"swap_ms": swap_ms, "swap_bytes_per_rank": stats["bytesExchanged"],
+                 "swap_share": swap_ms / (1e3 * elapsed) if elapsed > 0 else None,
+                 "swap_GBps_per_rank": (stats["bytesExchanged"] / (swap_ms * 1e-3) / 1e9) if swap_ms > 0 else None}
     result = {
         "metric": "single-qubit-gate time (s) vs #qubits, fp64 state-vector; 1/2/4/8-GPU scaling",
         "value": s_per_gate,
@@ -160,12 +207,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": s_per_gate / BASELINE_S_PER_OP,
         "dtype": "fp64" if qa.capi.binding().prec == 2 else "fp32",
-        "data": "synthetic: |+>^n initial state, seeded random layered circuit",
+        "data": "synthetic: |+>^n initial state, seeded random layered circuits (one window per seed), random angles",
         "config": {
-            "model": f"random layered circuit (1q gate on every qubit + CNOT brick), {n} qubits",
+            "model": f"random layered circuits (1q gate on every qubit + CNOT brick), {n} qubits, "
+                     f"seeds {','.join(map(str, seeds))}",
             "qubits": n,
             "qubits_per_gpu": args.qubits,
-            "global_batch": 1,
+            "global_batch": len(seeds),
             "seq_len": 1 << n,
             "gates_per_step": gates / max(args.steps, 1),
             "parallelism": f"dp{world}: amplitude-sharded over {world} GPU(s)" +
@@ -173,9 +221,14 @@ def main():
                             ("RCCL" if transport.startswith("RCCL") else transport)),
             "transport": transport,
             "fusion": not args.eager,
+            "value_is": "mean s/gate over the seeds' windows (total time / total gates)",
+            "seeds": seed_rows,
+            "seed7_s_per_gate": next((r["s_per_gate"] for r in seed_rows if r["seed"] == 7), None),
             "passes": stats["passes"],
+            "passes_per_seed": stats["passes"] / len(seeds),
             "swaps": stats["swaps"],
-            "norm_error": abs(norm - 1.0),
+            **multi,
+            "norm_error": max(abs(norm - 1.0), norm_err),
             "unfused_gate_s": unfused_gate_s,
             "backend": qa.capi.getQuESTBackend(),
             **extras,
@@ -194,12 +247,12 @@ def _median_time(fn, reps=5):
     return sorted(ts)[len(ts) // 2]
 
 
-def run_extras(qa, reg, n, layer_gates, args):
+def run_extras(qa, reg, n, layer_gates, args, seed):
     """Single-GPU extras, outside the timed region (see the module
     docstring); closes the bench register before the 256 GiB ones."""
     from quest_amd.models import fork_circuit
     from quest_amd.models.circuits import Circuit
-    from quest_amd.utils.bench_workloads import run_density17, run_q34
+    from quest_amd.utils.bench_workloads import run_density17, run_q34, run_rotate29
 
     todo = set(args.extras.split(","))
     out = {}
@@ -264,6 +317,9 @@ def run_extras(qa, reg, n, layer_gates, args):
         qa.capi.setGateFusion(1)
         out["sweep"] = sweep
 
+    if "rotate29" in todo:
+        res29 = {}
+        guarded("rotate29", lambda: (run_rotate29(reg.envobj, res29), out.__setitem__("rotate29", res29["rotate29"])))
     if "window1" in todo:
         guarded("window1", window1)
     if "fork30" in todo:
@@ -280,17 +336,17 @@ def run_extras(qa, reg, n, layer_gates, args):
         if "density17" in todo:
             guarded("density17", lambda: (run_density17(env, res), out.__setitem__("density17", res["density17"])))
     if "fp32" in todo and qa.capi.binding().prec == 2:
-        guarded("fp32", lambda: out.__setitem__("fp32", _run_fp32(args)))
+        guarded("fp32", lambda: out.__setitem__("fp32", _run_fp32(args, seed)))
     return out
 
 
-def _run_fp32(args):
+def _run_fp32(args, seed):
     """The headline circuit with the fp32 library, in a child process (a
     process binds one native library)."""
     import subprocess
 
     cmd = [sys.executable, os.path.abspath(__file__), "--no-extras", "--steps", str(args.steps), "--warmup",
-           str(args.warmup), "--qubits", str(args.qubits), "--seed", str(args.seed)]
+           str(args.warmup), "--qubits", str(args.qubits), "--seed", str(seed)]
     env = dict(os.environ, QUEST_PREC="1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)

@@ -144,6 +144,7 @@ typedef struct QuESTStats {
                                  computed by the permuted kernels without a relayout */
     long long relayouts;      /* canonicalisations that moved data (getAmps, file IO, ... after relabelling) */
     long long restoreRounds;  /* concurrent rounds of whole-chunk exchanges restoring the chunk placement */
+    long long swapMicros;     /* device time of the qubit swaps (HIP: events on the compute stream; reading waits for them) */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

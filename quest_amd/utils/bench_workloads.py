@@ -147,6 +147,49 @@ def run_fork30(env, res):
     r.close()
 
 
+# the reference's per-target benchmark (tests/benchmarks/rotate_benchmark.test:8-57):
+# compactUnitary with the first angle triple on every target of a 29-qubit
+# |0...0> register, 20 trials per target
+ROTATE_ANGLES = (1.2320, 0.4230, -0.6523)
+
+
+def run_rotate29(env, res, n=29, trials=20):
+    """compactUnitary on every target, each trial synced (the reference's CPU
+    library returns when the gate is done; a GPU call returns at launch), with
+    mean / stdev / min / max per target and the achieved HBM rate against the
+    2^(n+5)-byte streaming floor of one read + one write of the state."""
+    import math
+
+    import quest_amd as qa
+
+    a = ROTATE_ANGLES
+    alpha = complex(math.cos(a[0]) * math.cos(a[1]), math.cos(a[0]) * math.sin(a[1]))
+    beta = complex(math.sin(a[0]) * math.cos(a[2]), math.sin(a[0]) * math.sin(a[2]))
+    q = qa.Register(env, n)
+    q.init_zero()
+    q.sync()
+    nbytes = 2 * 16 * (1 << n)
+    rows = []
+    for t in range(n):
+        q.compact(t, alpha, beta)   # warm this target's kernel
+        q.sync()
+        ts = []
+        for _ in range(trials):
+            t0 = time.perf_counter()
+            q.compact(t, alpha, beta)
+            q.sync()
+            ts.append(time.perf_counter() - t0)
+        mean = statistics.mean(ts)
+        rows.append({"target": t, "mean_ms": 1e3 * mean, "stdev_ms": 1e3 * statistics.stdev(ts),
+                     "min_ms": 1e3 * min(ts), "max_ms": 1e3 * max(ts), "TBps": nbytes / mean / 1e12})
+    norm = q.total_prob()
+    q.close()
+    means = [r["mean_ms"] for r in rows]
+    res["rotate29"] = {"qubits": n, "trials": trials, "bytes_per_gate": nbytes, "per_target": rows,
+                       "mean_ms": statistics.mean(means), "slowest_ms": max(means), "fastest_ms": min(means),
+                       "spread": max(means) / min(means), "norm_error": abs(norm - 1.0)}
+
+
 def run_q34(env, res, n=34):
     import quest_amd as qa
     from quest_amd.models import random_layered

@@ -1197,9 +1197,13 @@ void getQuESTStats(QuESTStats* s) {
     s->permutedOps = stats().permutedOps;
     s->relayouts = stats().relayouts;
     s->restoreRounds = stats().restoreRounds;
+    s->swapMicros = be::swapMicros(true);
 }
 
-void resetQuESTStats(void) { stats() = Stats(); }
+void resetQuESTStats(void) {
+    stats() = Stats();
+    be::swapMicrosReset();
+}
 
 const char* getQuESTTransport(void) {
     static std::string d;

@@ -20,7 +20,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
-#include <algorithm>
 #include <string>
 #include <thread>
 #include <vector>
@@ -202,8 +201,12 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
         // that does not greet like rank 0, and retry.
         // (rank 0 greets when it reaches this rendezvous: wait long enough for
         // a rank 0 still busy with device or RCCL initialisation)
+        // (each attempt waits at most 60 s, and never past the budget, so a
+        // connection that lands on a listener that never greets is retried)
+        const double left =
+            timeoutSeconds() - std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !selfConnected(fd) &&
-            readGreeting(fd, std::max(60.0, timeoutSeconds())))
+            readGreeting(fd, std::max(1.0, std::min(60.0, left))))
             break;
         close(fd);
         double waited =

@@ -42,6 +42,7 @@ struct Imported {
     unsigned long long id;
     char* ptr;
     unsigned long long lastUse;
+    bool state = false;   // a peer's state array (mapArrays): closed again by done()
 };
 std::vector<Imported> g_imported;
 unsigned long long g_clock = 0;
@@ -237,8 +238,11 @@ void mapArrays(const int* peers, int n, void* const* arrays, int nArr, void** ou
     }
     for (int i = 0; i < n; i++) {
         sock::sendrecv(peers[i], mine.data(), theirs.data(), sizeof(Token) * (size_t)nArr);
-        for (int a = 0; a < nArr; a++)
+        for (int a = 0; a < nArr; a++) {
             out[(size_t)i * nArr + a] = importBuffer(peers[i], theirs[(size_t)a]) + theirs[(size_t)a].offset;
+            for (Imported& m : g_imported)
+                if (m.peer == peers[i] && m.id == theirs[(size_t)a].id) m.state = true;
+        }
     }
 }
 
@@ -248,6 +252,18 @@ void done(const int* peers, int n, hipStream_t producer) {
     for (int i = 0; i < n; i++) {
         int a = 1, b = 0;
         sock::sendrecv(peers[i], &a, &b, sizeof a);
+    }
+    // Unmap the peers' state arrays now that our swap kernels are done with
+    // them: a mapping kept until the peer's next token would pin a register
+    // the peer may destroy meanwhile, and a destroy-then-create of a register
+    // of the same size could then run out of device memory.
+    for (size_t i = 0; i < g_imported.size();) {
+        if (g_imported[i].state) {
+            QA_HIP_CHECK(hipIpcCloseMemHandle(g_imported[i].ptr));
+            g_imported.erase(g_imported.begin() + (long)i);
+        } else {
+            i++;
+        }
     }
 }
 

@@ -104,5 +104,15 @@ void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* bufRe, const real* b
 void bufferToHost(const real* buf, real* host, i64 n);
 void hostToBuffer(const real* host, real* buf, i64 n);
 
+// ---- swap timing (QuESTStats.swapMicros) --------------------------------------
+// swapMark(true) / swapMark(false) bracket one qubit swap on the device
+// timeline (HIP: events on the compute stream, so the interval starts when the
+// passes queued before the swap have run; host build: wall clock).
+// swapMicros(drain) returns the total of the completed intervals, waiting for
+// pending ones when drain is set; swapMicrosReset() clears it.
+void swapMark(bool begin);
+long long swapMicros(bool drain);
+void swapMicrosReset();
+
 }  // namespace be
 }  // namespace qa

@@ -49,20 +49,23 @@ namespace {
 struct XBuf {
     std::vector<real*> send, recv;
     i64 amps = 0;  // capacity per buffer in amplitudes (per re/im half)
+    bool hasSend = false;
 } g_x;
 
-void ensureXBuf(int peers, i64 amps) {
-    if ((int)g_x.send.size() >= peers && g_x.amps >= amps) return;
+// withSend = false: receive buffers only (RCCL sends straight from the state)
+void ensureXBuf(int peers, i64 amps, bool withSend = true) {
+    if ((int)g_x.recv.size() >= peers && g_x.amps >= amps && (g_x.hasSend || !withSend)) return;
     be::deviceSync();  // the communication stream may still read the old buffers
-    for (real* p : g_x.send) be::freeComm(p);
+    for (real* p : g_x.send) if (p) be::freeComm(p);
     for (real* p : g_x.recv) be::freeComm(p);
     g_x.send.assign(peers, nullptr);
     g_x.recv.assign(peers, nullptr);
     for (int i = 0; i < peers; i++) {
-        g_x.send[i] = (real*)be::allocComm(sizeof(real) * 2 * amps);
+        if (withSend) g_x.send[i] = (real*)be::allocComm(sizeof(real) * 2 * amps);
         g_x.recv[i] = (real*)be::allocComm(sizeof(real) * 2 * amps);
     }
     g_x.amps = amps;
+    g_x.hasSend = withSend;
 }
 
 inline int chunkBit(const QuregImpl& q, int phys) { return (q.chunkId >> (phys - q.L)) & 1; }
@@ -135,6 +138,7 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     if (k <= 0) return;
     be::flush(q);
     trace::Range range("quest.swap");
+    be::swapMark(true);
     const double t0 = trace::now();
     const long long bytes0 = stats().bytesExchanged;
     // order by rank bit so that peers come in increasing (peer ^ rank) order
@@ -155,7 +159,18 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     // two buffer sets: slice s is packed into set s & 1 and exchanged on the
     // communication stream while slice s - 1 is unpacked and s + 1 packed
     const int np = parts - 1;
-    if (!comm::swapsInPlace()) ensureXBuf(2 * np, slice);
+    // the swapped local bits are the top k local positions: part j of the
+    // chunk is one contiguous range (its first amplitude index is setMask[j]),
+    // sent straight from the state -- no pack, one HBM round trip of 7/8 of
+    // the chunk fewer (transports that send from any device memory; RCCL)
+    bool direct = false;   // parts sent straight from the state
+    if (!comm::swapsInPlace()) {
+        bool top = comm::sendsFromState();
+        for (int m = 0; m < k; m++) top = top && lpos[m] >= q.L - k;
+        static const bool directOn = !getenv("QUEST_SWAP_DIRECT") || atoi(getenv("QUEST_SWAP_DIRECT")) != 0;
+        direct = top && directOn;
+        ensureXBuf(2 * np, slice, !direct);
+    }
     std::vector<comm::Xfer> xs[2] = {std::vector<comm::Xfer>(np), std::vector<comm::Xfer>(np)};
     std::vector<u64> setMask(parts);
     for (int j = 0; j < parts; j++) {
@@ -164,7 +179,6 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
             if ((j >> m) & 1) msk |= 1ull << lpos[m];
         setMask[j] = msk;
     }
-    bool direct = false;   // parts sent straight from the state
     if (comm::swapsInPlace()) {
         // IPC: the two parts of each rank pair are swapped in place through
         // the peer's mapped state (no buffers; every amplitude read and
@@ -192,14 +206,6 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         stats().bytesExchanged += (long long)(sizeof(real) * 2 * partSize) * np;
     } else {
         const i64 nSlices = (partSize + slice - 1) / slice;
-        // the swapped local bits are the top k local positions: part j of the
-        // chunk is one contiguous range (its first amplitude index is setMask[j]),
-        // sent straight from the state -- no pack, one HBM round trip of 7/8 of
-        // the chunk fewer (transports that send from any device memory; RCCL)
-        bool top = comm::sendsFromState();
-        for (int m = 0; m < k; m++) top = top && lpos[m] >= q.L - k;
-        static const bool directOn = !getenv("QUEST_SWAP_DIRECT") || atoi(getenv("QUEST_SWAP_DIRECT")) != 0;
-        direct = top && directOn;
         if (direct)
             for (int b = 0; b < 2; b++) xs[b].resize((size_t)(2 * np));
         auto unpack = [&](i64 s) {
@@ -240,6 +246,7 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         comm::exchangeWait((int)((nSlices - 1) & 1));
         unpack(nSlices - 1);
     }
+    be::swapMark(false);
     char moved[128];
     int at = 0;
     moved[0] = 0;
@@ -555,7 +562,9 @@ MemoryPlan memoryPlan(int nSV, int numRanks) {
     MemoryPlan m;
     m.state = 2ll * (long long)sizeof(real) << L;
     // multiSwap with k rank qubits: 2 (send, recv) x 2 (double buffer) x
-    // (2^k - 1) peers x slice amps x [re | im]; restoreChunks: one peer
+    // (2^k - 1) peers x slice amps x [re | im]; restoreChunks: one peer.
+    // An upper bound: RCCL swaps of top-position parts allocate the receive
+    // buffers only, and in-place IPC swaps none.
     const i64 partMax = (i64)1 << L;
     for (int k = 1; k <= g; k++) {
         i64 slice = (rt().exchangeSliceBytes >> (k - 1)) / (i64)(2 * sizeof(real));
@@ -609,7 +618,9 @@ bool footprintCheck(int nSV, int numRanks, std::string& report) {
              nSV, numRanks, m.state / G, 2.0 * 2 * np * bytes / G, 2 * np, bytes / 1048576.0, g, m.scratch / G,
              m.total / G, tot / G, f0 / G, f1 / G, known ? "" : " (unknown)");
     report = std::string(head) + r;
-    return ok && (long long)(2 * 2 * np * bytes) == m.exchange;
+    // the plan is an upper bound: its maximum can come from a k < g term or
+    // the chunk restore, and direct / in-place swaps allocate less
+    return ok && (long long)(2 * 2 * np * bytes) <= m.exchange;
 }
 
 void create(QuregImpl& q, int nSV, bool density) {

@@ -512,6 +512,26 @@ int& diagAsPhases() {
     return v;
 }
 
+// QUEST_PLAN_COMMUTE=1: class-aware commutation in the pass scheduler; 0
+// (default) the round-4 rule: ops touching a common bit never pass each other
+// unless both touch it diagonally as controls / phase masks.  Over 15 bench
+// seeds the greedy planner made 254 passes with it and 251 without (per seed
+// -4 .. +4): more freedom per pass does not make the greedy plan better.
+bool planCommute() {
+    static const bool v = getenv("QUEST_PLAN_COMMUTE") && atoi(getenv("QUEST_PLAN_COMMUTE")) != 0;
+    return v;
+}
+
+// 0: diagonal 2x2, 1: a I + b X, 2: anything else (multi-target ops too)
+int commuteClass(const Op& op) {
+    if (op.kind != OpKind::Mat2) return op.kind == OpKind::Diag ? 0 : 2;
+    auto zero = [](cplx z) { return z.re == 0 && z.im == 0; };
+    auto same = [](cplx a, cplx b) { return a.re == b.re && a.im == b.im; };
+    if (zero(op.m[1]) && zero(op.m[2])) return 0;
+    if (same(op.m[0], op.m[3]) && same(op.m[1], op.m[2])) return 1;
+    return 2;
+}
+
 void applyPerm(std::vector<Op>& ops, const std::vector<char>& done, int first, const int* pi) {
     for (int i = first; i < (int)ops.size(); i++)
         if (!done[i]) remapOp(ops[i], pi);
@@ -566,17 +586,38 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
     int first = 0;
     std::vector<int> take, best;
     const int maxOps = planMaxOps();
+    // Commutation classes of one-target ops (QUEST_PLAN_COMMUTE=1): a
+    // diagonal 2x2 (Z, S, T, Rz, phase shifts) commutes with controls and with
+    // other diagonals on its target; an "X-class" 2x2 (a I + b X: X, Rx, the X
+    // of CNOT / Toffoli) commutes with other X-class ops on its target, whatever
+    // their controls (on every control configuration both act as commuting
+    // 2x2s or not at all).  Anything else, and multi-target ops, conflicts with
+    // every deferred op touching its targets.
+    std::vector<unsigned char> cls(n, 2);   // 0 diagonal, 1 X-class, 2 general
+    const bool commute = planCommute();
+    if (commute)
+        for (int i = 0; i < n; i++) cls[i] = (unsigned char)commuteClass(ops[i]);
     // one greedy scan from `first` with the high bits `preset` claimed up front
     auto scan = [&](u64 preset, std::vector<int>& picked) {
         picked.clear();
         u64 high = preset;
         u64 blockedTg = 0;      // targets of ops deferred past this pass
         u64 blockedTouch = 0;   // targets | controls of deferred ops
+        // (class-aware) deferred targets of diagonal / X-class / general ops,
+        // and deferred controls and phase masks
+        u64 bD = 0, bX = 0, bG = 0, bC = 0;
         for (int i = first; i < n; i++) {
             if (done[i]) continue;
             const u64 tg = targetMask(ops[i]);
             const u64 touch = tg | ops[i].ctrl;
-            const bool free = !(tg & blockedTouch) && !(touch & blockedTg);
+            bool free;
+            if (commute) {
+                const int k2 = cls[i];
+                const u64 hitT = k2 == 0 ? (bX | bG) : k2 == 1 ? (bD | bC | bG) : (bD | bX | bG | bC);
+                free = !(tg & hitT) && !(ops[i].ctrl & (bX | bG));
+            } else {
+                free = !(tg & blockedTouch) && !(touch & blockedTg);
+            }
             const u64 need = high | (tg & ~low);
             if (free && popcount64(need) <= highSlots && (maxOps <= 0 || (int)picked.size() < maxOps)) {
                 high = need;
@@ -584,6 +625,10 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             } else {
                 blockedTg |= tg;
                 blockedTouch |= touch;
+                if (commute) {
+                    (cls[i] == 0 ? bD : cls[i] == 1 ? bX : bG) |= tg;
+                    bC |= ops[i].ctrl;
+                }
             }
         }
         return high;

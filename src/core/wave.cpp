@@ -1636,7 +1636,8 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         }
     }
     if (!t_planQuiet)
-        for (size_t o = trBeforeStore; o < out.ops.size(); o++) g_waveStoreTrCost += waveTransposeCost(out.ops[o].b);
+        for (size_t o = trBeforeStore; o < out.ops.size(); o++)
+            if (out.ops[o].kind == (int)WKind::TR) g_waveStoreTrCost += waveTransposeCost(out.ops[o].b);
     // flips still pending: folded into the store offsets
     wp.stFlip = slotFlips();
     wp.stFlipLane = laneFlips();

@@ -5,6 +5,7 @@
 // obviously-correct loops, so every layer above the kernels (front-end,
 // router, RCCL-style swaps, fusion planner) is testable on CPU.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -346,6 +347,25 @@ int fuseQubits() {
 void envInit(int, int, int) {}
 void envFinalize() {}
 void deviceSync() {}
+
+namespace {
+std::chrono::steady_clock::time_point g_swapT0;
+long long g_swapUs = 0;
+bool g_swapOpen = false;
+}  // namespace
+
+void swapMark(bool begin) {
+    const auto now = std::chrono::steady_clock::now();
+    if (begin) {
+        g_swapT0 = now;
+        g_swapOpen = true;
+    } else if (g_swapOpen) {
+        g_swapUs += std::chrono::duration_cast<std::chrono::microseconds>(now - g_swapT0).count();
+        g_swapOpen = false;
+    }
+}
+long long swapMicros(bool) { return g_swapUs; }
+void swapMicrosReset() { g_swapUs = 0; }
 std::string describe() { return "host C++ (plumbing build, no GPU)"; }
 const char* shortName() { return "CPU"; }
 bool stateOnHost() { return true; }

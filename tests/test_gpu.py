@@ -409,6 +409,53 @@ def test_ipc_in_place_swaps_fp32(genv, tmp_path, ranks):
     assert np.max(np.abs(a - b)) < 2e-6
 
 
+IPC_RELEASE = r'''
+import json, sys
+import torch
+import quest_amd as qa
+from quest_amd.ops import capi
+env = qa.Env()
+torch.cuda.init()
+env.sync()
+free0 = torch.cuda.mem_get_info()[0]
+frees = []
+for it in range(3):
+    r = qa.Register(env, 31)          # 16 GiB per rank, both ranks on this device
+    r.init_plus()
+    for q in range(31):
+        r.h(q)                         # the top qubit is the rank qubit: a swap
+    r.cnot(30, 0)
+    assert abs(r.total_prob() - 1) < 1e-9
+    r.close()
+    env.sync()
+    frees.append(torch.cuda.mem_get_info()[0])
+st = capi.getQuESTStats()
+if env.rank == 0:
+    print("STATS " + json.dumps({"free0": free0, "frees": frees, "swaps": st["swaps"]}))
+'''
+
+
+def test_ipc_state_mappings_released_after_swaps(genv, tmp_path):
+    """In-place IPC swaps map the peer's whole state; the mappings are closed
+    when the swap completes (comm_ipc.cpp done()), so a destroyed register's
+    memory returns to the device at once and destroy / create loops at large
+    sizes do not accumulate pinned allocations (round-4 advisor finding)."""
+    from quest_amd.parallel import spawn_local
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    base = {"QUEST_BACKEND": "hip", "PYTHONPATH": os.path.dirname(here)}
+    res = spawn_local(["-c", IPC_RELEASE], 2, env_extra=dict(base, QUEST_COMM="ipc", QUEST_COMM_TIMEOUT="120"),
+                      timeout=240)
+    for r, q in enumerate(res):
+        assert q.returncode == 0, f"rank {r}:\n{q.stdout[-1500:]}\n{q.stderr[-2500:]}"
+    st = json.loads([ln for ln in res[0].stdout.splitlines() if ln.startswith("STATS")][0][6:])
+    assert st["swaps"] >= 3, st
+    gib = 1 << 30
+    # each 16 GiB chunk (32 GiB of states over both ranks) is back after every destroy
+    for f in st["frees"]:
+        assert f > st["free0"] - 3 * gib, st
+
+
 def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
     """The fork's 30-qubit benchmark program (examples/random_circuit_benchmark.c
     flow: 490 gates, then P(q_i=1) for all 30 qubits and 10 amplitudes) on the
