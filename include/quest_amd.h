@@ -145,6 +145,8 @@ typedef struct QuESTStats {
     long long relayouts;      /* canonicalisations that moved data (getAmps, file IO, ... after relabelling) */
     long long restoreRounds;  /* concurrent rounds of whole-chunk exchanges restoring the chunk placement */
     long long swapMicros;     /* device time of the qubit swaps (HIP: events on the compute stream; reading waits for them) */
+    long long overlappedSwaps;  /* swaps run on a stream of their own, next to gate passes (QUEST_SWAP_OVERLAP) */
+    long long overlappedPasses; /* passes started on the part of the chunk a swap in flight leaves in place */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

@@ -1198,6 +1198,8 @@ void getQuESTStats(QuESTStats* s) {
     s->relayouts = stats().relayouts;
     s->restoreRounds = stats().restoreRounds;
     s->swapMicros = be::swapMicros(true);
+    s->overlappedSwaps = stats().overlappedSwaps;
+    s->overlappedPasses = stats().overlappedPasses;
 }
 
 void resetQuESTStats(void) {

@@ -52,6 +52,10 @@ void exchange(const Xfer* x, int n);
 // (0 or 1).  Stream-less transports finish inside exchangeAsync.
 void exchangeAsync(const Xfer* x, int n, int slot);
 void exchangeWait(int slot);
+// Whether exchangeAsync / exchangeWait are stream-ordered device operations
+// without host waits (RCCL): a swap built from them can run on a stream of
+// its own, next to gate passes (overlapped swaps, router multiSwap).
+bool exchangeStreamOrdered();
 // Whether the transport can send from any device memory (RCCL: the state
 // itself), not only from comm buffers (IPC exports them, sockets stage them).
 bool sendsFromState();

@@ -27,6 +27,7 @@ void exchange(const Xfer* x, int n) {
 }
 void exchangeAsync(const Xfer* x, int n, int) { exchange(x, n); }
 bool sendsFromState() { return false; }
+bool exchangeStreamOrdered() { return false; }
 bool swapsInPlace() { return false; }
 void mapPeerArrays(const int*, int, void* const*, int, void**) {
     fprintf(stderr, "QuEST: in-place peer swaps need the device IPC transport\n");

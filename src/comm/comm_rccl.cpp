@@ -342,6 +342,7 @@ void socketExchange(const Xfer& x) {
 }  // namespace
 
 void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
+    hipk::settleSwaps();   // an overlapped swap's transfers come first on every rank
     if (peer == g_rank) {
         QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, S()));
         return;
@@ -354,6 +355,7 @@ void sendrecv(int peer, const void* send, void* recv, size_t bytes) {
 }
 
 void exchange(const Xfer* x, int n) {
+    hipk::settleSwaps();   // an overlapped swap's transfers come first on every rank
     if (g_mode == Mode::Socket || g_mode == Mode::Single) {
         for (int i = 0; i < n; i++) sendrecv(x[i].peer, x[i].send, x[i].recv, x[i].bytes);
         return;
@@ -380,6 +382,8 @@ bool pipelined() {
     static const bool off = getenv("QUEST_EXCHANGE_PIPELINE") && atoi(getenv("QUEST_EXCHANGE_PIPELINE")) == 0;
     return !off && (g_mode == Mode::Rccl || g_mode == Mode::Ipc) && g_cstream;
 }
+
+bool exchangeStreamOrdered() { return g_mode == Mode::Rccl && pipelined(); }
 
 void exchangeAsync(const Xfer* x, int n, int slot) {
     if (!pipelined()) {
@@ -431,6 +435,7 @@ void rcclBcast(void* buf, size_t bytes, int root) {
 }  // namespace
 
 void allreduceSum(double* vals, int n) {
+    hipk::settleSwaps();   // an overlapped swap's transfers come first on every rank
     if (g_size == 1) return;
     if (g_mode == Mode::Socket || g_mode == Mode::Ipc) {
         sock::allreduceSum(vals, n);
@@ -440,12 +445,14 @@ void allreduceSum(double* vals, int n) {
 }
 
 int allreduceAnd(int v) {
+    hipk::settleSwaps();   // an overlapped swap's transfers come first on every rank
     double d = v ? 0.0 : 1.0;
     allreduceSum(&d, 1);
     return d == 0.0 ? 1 : 0;
 }
 
 void bcastHost(void* buf, size_t bytes, int root) {
+    hipk::settleSwaps();   // an overlapped swap's transfers come first on every rank
     if (g_size == 1) return;
     if (g_mode == Mode::Socket || g_mode == Mode::Ipc) {
         sock::bcastHost(buf, bytes, root);
@@ -455,6 +462,7 @@ void bcastHost(void* buf, size_t bytes, int root) {
 }
 
 void allgather(const void* send, void* recv, size_t bytesPerRank) {
+    hipk::settleSwaps();   // an overlapped swap's transfers come first on every rank
     if (g_size == 1) {
         QA_HIP_CHECK(hipMemcpyAsync(recv, send, bytesPerRank, hipMemcpyDeviceToDevice, S()));
         return;
@@ -473,6 +481,7 @@ void allgather(const void* send, void* recv, size_t bytesPerRank) {
 }
 
 void barrier() {
+    hipk::settleSwaps();   // an overlapped swap's transfers come first on every rank
     double d = 1;
     allreduceSum(&d, 1);
 }

@@ -104,6 +104,31 @@ void fromBuffer(QuregImpl& q, i64 local, i64 n, const real* bufRe, const real* b
 void bufferToHost(const real* buf, real* host, i64 n);
 void hostToBuffer(const real* host, real* buf, i64 n);
 
+// ---- overlapped swaps ----------------------------------------------------------
+// swapOverlapBegin(q, lpos, k, myG), right after the pre-swap flush: the
+// swap's packs / unpacks (and the transport's stream-ordered exchanges) go to
+// a stream of their own, started after everything queued so far; returns
+// false (nothing changed) if this backend or configuration cannot overlap.
+// swapOverlapEnd(q): the swap is issued.  Until it is settled, passes of q
+// whose tiles avoid the swapped local positions lpos run at once on the part
+// of the chunk the swap leaves in place (local bits lpos = myG) and their
+// other parts are deferred; the first operation that needs the whole chunk
+// (any other backend call on q, a pass that includes an lpos, a device sync)
+// waits for the swap and runs the deferred parts first, in order.
+bool swapOverlapBegin(QuregImpl& q, const int* lpos, int k, int myG);
+void swapOverlapEnd(QuregImpl& q);
+// Before the pre-swap flush (router planSwap, victims chosen ahead of it and
+// kept out of tiles through q.tileAvoid): passes of q launched from now until
+// swapOverlapBegin whose tiles avoid lpos run at once on the parts the swap
+// sends (local bits lpos != myG) -- so the sends can start -- and on the part
+// it keeps only once the swap has been issued, next to the transfer.  False
+// if this backend does not split (nothing changed).
+bool preSwap(QuregImpl& q, const int* lpos, int k, int myG);
+// Local positions the ops queued for q target, plus the low positions every
+// planned tile holds: swap victims outside them are never a tile bit of the
+// passes that flush plans.
+u64 queuedTargets(const QuregImpl& q);
+
 // ---- swap timing (QuESTStats.swapMicros) --------------------------------------
 // swapMark(true) / swapMark(false) bracket one qubit swap on the device
 // timeline (HIP: events on the compute stream, so the interval starts when the

@@ -100,6 +100,9 @@ struct QuregImpl {
     // default), kept until the queue has drained
     int planStrategy = -1;
     std::future<int> strategySearch;
+    // local positions the planner keeps out of tile padding (router planSwap:
+    // the victims of the swap being prepared; 0 otherwise)
+    u64 tileAvoid = 0;
     bool permIdentity() const {
         for (int i = 0; i < nSV; i++)
             if (l2p[i] != i) return false;

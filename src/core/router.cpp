@@ -134,6 +134,20 @@ void enqueue(QuregImpl& q, const Op& op) {
 // reference's pairwise half-chunk exchange; swapping all rank qubits at once
 // uses every link (QuEST_cpu_distributed.c:41-512 exchanges whole chunks,
 // pairwise, once per gate).
+// The swap's pairs ordered by rank bit (peers then come in increasing
+// (peer ^ rank) order) and this rank's part: local bits lpos = myG stay here.
+void swapOrder(const QuregImpl& q, const int* gposIn, const int* lposIn, int k, int* gpos, int* lpos, int* myG) {
+    int idx[8];
+    for (int m = 0; m < k; m++) idx[m] = m;
+    std::sort(idx, idx + k, [&](int a, int b) { return gposIn[a] < gposIn[b]; });
+    for (int m = 0; m < k; m++) {
+        gpos[m] = gposIn[idx[m]];
+        lpos[m] = lposIn[idx[m]];
+    }
+    *myG = 0;
+    for (int m = 0; m < k; m++) *myG |= chunkBit(q, gpos[m]) << m;
+}
+
 void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     if (k <= 0) return;
     be::flush(q);
@@ -141,16 +155,8 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
     be::swapMark(true);
     const double t0 = trace::now();
     const long long bytes0 = stats().bytesExchanged;
-    // order by rank bit so that peers come in increasing (peer ^ rank) order
-    int gpos[8], lpos[8], idx[8];
-    for (int m = 0; m < k; m++) idx[m] = m;
-    std::sort(idx, idx + k, [&](int a, int b) { return gposIn[a] < gposIn[b]; });
-    for (int m = 0; m < k; m++) {
-        gpos[m] = gposIn[idx[m]];
-        lpos[m] = lposIn[idx[m]];
-    }
-    int myG = 0;
-    for (int m = 0; m < k; m++) myG |= chunkBit(q, gpos[m]) << m;
+    int gpos[8], lpos[8], myG;
+    swapOrder(q, gposIn, lposIn, k, gpos, lpos, &myG);
     const int parts = 1 << k;
     const i64 partSize = q.numAmpsPerChunk >> k;
     i64 slice = (rt().exchangeSliceBytes >> (k - 1)) / (i64)(2 * sizeof(real));
@@ -171,6 +177,12 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         direct = top && directOn;
         ensureXBuf(2 * np, slice, !direct);
     }
+    // Overlapped swap (stream-ordered transports, backend.hpp): the exchange
+    // runs on a stream of its own next to the passes on the part of the chunk
+    // it leaves in place (local bits lpos = myG) -- those planned before it
+    // (be::preSwap) and after it; the reference's exchange blocks
+    // (QuEST_cpu_distributed.c:451-479)
+    const bool overlap = !comm::swapsInPlace() && comm::exchangeStreamOrdered() && be::swapOverlapBegin(q, lpos, k, myG);
     std::vector<comm::Xfer> xs[2] = {std::vector<comm::Xfer>(np), std::vector<comm::Xfer>(np)};
     std::vector<u64> setMask(parts);
     for (int j = 0; j < parts; j++) {
@@ -247,6 +259,7 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
         unpack(nSlices - 1);
     }
     be::swapMark(false);
+    if (overlap) be::swapOverlapEnd(q);
     char moved[128];
     int at = 0;
     moved[0] = 0;
@@ -438,12 +451,51 @@ void restoreChunks(QuregImpl& q) {
 // every rank qubit the queue still targets comes in, in order of first use,
 // displacing the local qubits whose first use lies furthest ahead (Belady),
 // as long as that is later than the incoming qubit's.
+// victims (local qubits to move out) for the qubits in[] the queue needs:
+// furthest next locality-requiring use first; 0 if one of them sits on a
+// position in `busy`; gp / lp as multiSwap takes them
+int chooseVictims(QuregImpl& q, const std::vector<Op>& lq, u64 busy, int* gp, int* lp);
+
 void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
-    // run what the backend holds first: its passes may relabel local qubits
-    // (wave relabelling), and the positions chosen below must be the ones the
-    // swap moves (multiSwap's own flush would otherwise move whatever qubit a
-    // relabel put at the victim's old position -- a needless later swap)
+    // Victims chosen BEFORE the backend's queue is planned (QUEST_SWAP_EARLY,
+    // default on) when none of them sits on a position a queued op targets
+    // (nor on the low positions every tile holds).  The planner keeps those
+    // positions out of its tiles (q.tileAvoid), so its relabelling passes
+    // cannot move the victims, and the backend can split the pre-swap passes
+    // around the swap (be::preSwap): the parts the swap sends first, the part
+    // it keeps next to the transfer.  Without a victim outside the queue's
+    // targets: run what the backend holds first, then choose (its passes may
+    // relabel local qubits, and the positions must be the ones the swap moves
+    // -- multiSwap's own flush would otherwise move whatever qubit a relabel
+    // put at the victim's old position, a needless later swap).
+    static const bool early = !getenv("QUEST_SWAP_EARLY") || atoi(getenv("QUEST_SWAP_EARLY")) != 0;
+    int gp[8], lp[8], k = 0;
+    if (early) {
+        k = chooseVictims(q, lq, be::queuedTargets(q), gp, lp);
+        static const bool dbg = getenv("QUEST_SWAP_DEBUG") != nullptr;
+        if (dbg)
+            fprintf(stderr, "rank %d swap: victims chosen %s the flush (%zu ops queued)\n", rt().rank,
+                    k ? "before" : "after", q.pending.size());
+        if (k > 0) {
+            u64 avoid = 0;
+            for (int m = 0; m < k; m++) avoid |= 1ull << lp[m];
+            q.tileAvoid = avoid;
+            int gs[8], ls[8], myG;
+            swapOrder(q, gp, lp, k, gs, ls, &myG);
+            if (!comm::swapsInPlace() && comm::exchangeStreamOrdered()) be::preSwap(q, ls, k, myG);
+        }
+    }
     be::flush(q);
+    if (k == 0) k = chooseVictims(q, lq, 0, gp, lp);
+    if (k == 0) {
+        fprintf(stderr, "QuEST: no local qubit available for a distributed swap\n");
+        exit(EXIT_FAILURE);
+    }
+    multiSwap(q, gp, lp, k);
+    q.tileAvoid = 0;
+}
+
+int chooseVictims(QuregImpl& q, const std::vector<Op>& lq, u64 busy, int* gp, int* lp) {
     const int INF = 1 << 30;
     int first[64];
     for (int i = 0; i < 64; i++) first[i] = INF;
@@ -468,7 +520,7 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
     // victims on the top positions for direct sends -- moved which qubit the
     // next window needs back and added a swap, host-build study)
     std::stable_sort(out.begin(), out.end(), [&](int a, int b) { return first[a] > first[b]; });
-    int gp[8], lp[8], k = 0;
+    int k = 0;
     for (size_t i = 0; i < in.size() && i < out.size() && k < 8; i++) {
         const bool required = (need0 >> in[i]) & 1;
         if (!required && first[out[i]] < first[in[i]]) break;
@@ -476,11 +528,14 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
         lp[k] = q.l2p[out[i]];
         k++;
     }
-    if (k == 0) {
-        fprintf(stderr, "QuEST: no local qubit available for a distributed swap\n");
-        exit(EXIT_FAILURE);
-    }
-    multiSwap(q, gp, lp, k);
+    // (busy: the victims must all sit outside it -- they are the same logical
+    // qubits the choice after the flush would take, so the swap count does
+    // not change; else the caller chooses again after its flush: a filtered
+    // choice took victims needed sooner, 4 ranks x 26 qubits 2 -> 3-5 swaps
+    // per window on three of five bench seeds)
+    for (int m = 0; m < k; m++)
+        if ((busy >> lp[m]) & 1) return 0;
+    return k;
 }
 
 // Route the logical queue of a distributed register: issue, in commutation-

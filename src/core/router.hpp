@@ -101,6 +101,8 @@ struct Stats {
     long long permutedOps = 0;    // inner products / axpby of registers in different layouts, no relayout
     long long relayouts = 0;      // canonicalisations that moved data
     long long restoreRounds = 0;  // concurrent rounds of whole-chunk exchanges restoring chunk placement
+    long long overlappedSwaps = 0;   // swaps issued on their own stream (be::swapOverlapBegin)
+    long long overlappedPasses = 0;  // passes started on the part a swap in flight leaves in place
 };
 Stats& stats();
 

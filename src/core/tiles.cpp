@@ -18,11 +18,15 @@ u64 targetMask(const Op& op) {
 
 int popcount64(u64 x) { return __builtin_popcountll(x); }
 
-void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k, int cmin, TileProgram& out) {
+void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k, int cmin, TileProgram& out,
+              u64 avoid = 0) {
     TilePass ps;
     ps.k = k;
     // Q = low cmin bits + targets, padded with the lowest remaining bits
+    // (not the avoided ones, unless nothing else is left)
     u64 q = tmask | ((cmin >= 64) ? ~0ull : ((1ull << cmin) - 1));
+    for (int bit = 0; popcount64(q) < k && bit < L; bit++)
+        if (!((avoid >> bit) & 1)) q |= 1ull << bit;
     for (int bit = 0; popcount64(q) < k && bit < L; bit++) q |= 1ull << bit;
     ps.qmask = q;
     int n = 0;
@@ -554,9 +558,10 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
     int n = (int)ops.size();
 
     const bool ready = hooks && hooks->passReady;
+    const u64 avoid = hooks ? hooks->avoidMask : 0;
     if (!fuse) {
         for (int i = 0; i < n; i++) {
-            emitPass(ops, i, i + 1, targetMask(ops[i]), L, k, c, out);
+            emitPass(ops, i, i + 1, targetMask(ops[i]), L, k, c, out, avoid);
             if (ready) hooks->passReady(out, i, ops);
         }
         return;
@@ -645,7 +650,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             tmp.reserve(sel.size());
             for (int i : sel) tmp.push_back(ops[i]);
             TileProgram scratch;
-            emitPass(tmp, 0, (int)tmp.size(), high, L, k, c, scratch);
+            emitPass(tmp, 0, (int)tmp.size(), high, L, k, c, scratch, avoid);
             const TilePass& ps = scratch.passes.back();
             return hooks->passCost(ps, scratch.ops.data() + ps.opBegin);
         };
@@ -752,7 +757,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             order.push_back(ops[i]);
             done[i] = 1;
         }
-        emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out);
+        emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out, avoid);
         if (relabelFrom >= 0 && (int)best.size() >= 2 && (int)order.size() < n) {
             // candidate store permutations (none, by first use, by use count),
             // each judged by how many ops the greedy plan of the NEXT pass

@@ -182,6 +182,10 @@ struct PlanHooks {
     // knobs of the wave planner's strategy search (searchWavePlan)
     int seeds = 0;
     double lookahead = -1;
+    // local positions no tile may take as padding (the victims of a qubit
+    // swap about to run, router planSwap): passes whose ops do not target
+    // them then leave them out, so the swap can overlap those passes
+    u64 avoidMask = 0;
 };
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,

@@ -549,8 +549,9 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
     waveCostHooks(costed);
     const double M = costed.memCost > 0 ? costed.memCost : 12800.0;
     const int fuse = fuseBlockQubits();
-    double score[kNumStrategies];
+    double score[kNumStrategies], took[kNumStrategies] = {0};
     auto run = [&](int i) {
+        const auto tRun0 = std::chrono::steady_clock::now();
         QuietPlan quiet;
         fuseBlockQubits() = fuse;              // (thread-local)
         t_waveCframe = kStrategies[i].cframe;  // (thread-local)
@@ -572,6 +573,7 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
             score[i] = t;
         }
         t_waveCframe = -1;
+        took[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tRun0).count();
     };
     std::vector<std::thread> pool;
     const int nStrat = searchStrategies();
@@ -586,7 +588,7 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
     if (dbg) {
         fprintf(stderr, "search over %zu ops (%.1f ms):", ops.size(),
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tSearch0).count());
-        for (int i = 0; i < nStrat; i++) fprintf(stderr, " %.0f", score[i]);
+        for (int i = 0; i < nStrat; i++) fprintf(stderr, " %.0f (%.1f ms)", score[i], took[i]);
         fprintf(stderr, " -> %d\n", best);
     }
     return best;

@@ -366,6 +366,17 @@ void swapMark(bool begin) {
 }
 long long swapMicros(bool) { return g_swapUs; }
 void swapMicrosReset() { g_swapUs = 0; }
+
+bool swapOverlapBegin(QuregImpl&, const int*, int, int) { return false; }
+void swapOverlapEnd(QuregImpl&) {}
+bool preSwap(QuregImpl&, const int*, int, int) { return false; }
+
+u64 queuedTargets(const QuregImpl& q) {
+    u64 m = 0xffull;   // the always-resident low positions of every wave tile (cmin <= 8)
+    for (const Op& op : q.pending)
+        for (int j = 0; j < op.nt; j++) m |= 1ull << op.t[j];
+    return m;
+}
 std::string describe() { return "host C++ (plumbing build, no GPU)"; }
 const char* shortName() { return "CPU"; }
 bool stateOnHost() { return true; }
@@ -474,6 +485,7 @@ void flushImpl(QuregImpl& q, bool front) {
     // engine lowers -- the same plans (QUEST_PLAN_STREAM=0: the fallback below)
     static const bool streamOn = !getenv("QUEST_PLAN_STREAM") || atoi(getenv("QUEST_PLAN_STREAM")) != 0;
     PlanHooks hooks;
+    hooks.avoidMask = q.tileAvoid;
     hooks.relabelOk = [](const TilePass& ps, const TileOp* ops) { return waveLowers(ps, ops); };
     hooks.lowPerm = [](const TilePass& ps, const TileOp* ops, int c, int* sigma) {
         return waveLowPerm(ps, ops, c, sigma);

@@ -22,6 +22,10 @@ namespace hipk {
 [[noreturn]] void fatal(const char* expr, const char* err, const char* file, int line);
 
 hipStream_t stream();   // the backend's compute stream (RCCL ops are ordered on it too)
+// Order the compute stream after an overlapped swap still in flight
+// (be::swapOverlapBegin) and run its deferred pass parts; the transport calls
+// it before any other collective or exchange.
+void settleSwaps();
 int numCUs();
 
 // Wait until `ev` (nullptr: everything queued on the stream) has completed.

@@ -456,6 +456,59 @@ def test_ipc_state_mappings_released_after_swaps(genv, tmp_path):
         assert f > st["free0"] - 3 * gib, st
 
 
+OVERLAP = r'''
+import json, sys
+import numpy as np
+import quest_amd as qa
+from quest_amd.models import random_layered
+from quest_amd.ops import capi
+env = qa.Env()
+n = int(sys.argv[2])
+r = qa.Register(env, n)
+r.init_plus()
+capi.resetQuESTStats()
+random_layered(n, 12, seed=3).apply(r)
+r.sync()
+st = capi.getQuESTStats()
+p = [r.prob(q, 1) for q in (0, n - 1)]
+v = r.to_numpy()
+if env.rank == 0:
+    np.save(sys.argv[1], v)
+    print("STATS " + json.dumps({k: st[k] for k in ("swaps", "overlappedSwaps", "overlappedPasses")}))
+'''
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_overlapped_swaps_rccl_shared_gpu(genv, tmp_path, ranks):
+    """Overlapped swaps (QUEST_SWAP_OVERLAP, default on): RCCL ranks sharing
+    the GPU (QUEST_RCCL_SHARED_GPU=1, the RCCL path of a multi-GPU node) with
+    21 local qubits, where the passes after each all-to-all start on the part
+    of the chunk the swap leaves in place while the exchange runs on its own
+    stream; the state equals the single-rank run's and the split launches
+    really happened."""
+    from quest_amd.parallel import spawn_local
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    n = 21 + {2: 1, 4: 2}[ranks]
+    one, dist = str(tmp_path / "one.npy"), str(tmp_path / "dist.npy")
+    base = {"QUEST_BACKEND": "hip", "PYTHONPATH": os.path.dirname(here)}
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, "-c", OVERLAP, one, str(n)], env=dict(os.environ, **base), capture_output=True,
+                       text=True, timeout=200)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    res = spawn_local(["-c", OVERLAP, dist, str(n)], ranks,
+                      env_extra=dict(base, QUEST_COMM="rccl", QUEST_RCCL_SHARED_GPU="1", QUEST_COMM_TIMEOUT="150"),
+                      timeout=240)
+    for r, q in enumerate(res):
+        assert q.returncode == 0, f"rank {r}:\n{q.stdout[-1500:]}\n{q.stderr[-2500:]}"
+    st = json.loads([ln for ln in res[0].stdout.splitlines() if ln.startswith("STATS")][0][6:])
+    assert st["swaps"] >= 1 and st["overlappedSwaps"] >= 1 and st["overlappedPasses"] >= 1, st
+    a, b = np.load(one), np.load(dist)
+    assert np.max(np.abs(a - b)) < 1e-10
+
+
 def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
     """The fork's 30-qubit benchmark program (examples/random_circuit_benchmark.c
     flow: 490 gates, then P(q_i=1) for all 30 qubits and 10 amplitudes) on the

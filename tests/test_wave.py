@@ -66,6 +66,47 @@ def test_fp32_wave_kernel_every_gate_kind_gpu():
     assert "bad: []" in out.stdout and " wave 0 " not in out.stdout
 
 
+FP32_DENSITY = r'''
+import sys
+import numpy as np
+sys.path.insert(0, "tests")
+import quest_amd as qa
+from helpers import apply_random_ops, oracle_for, state_of
+from quest_amd.utils import oracle as O
+env = qa.Env()
+n = 10
+rng = np.random.default_rng(310)
+reg = qa.Register(env, n, density=True)
+o = oracle_for(reg, rng)
+qa.capi.resetQuESTStats()
+apply_random_ops(reg, o, rng, 30)
+for k in range(40):
+    a = int(rng.integers(n))
+    p = float(rng.uniform(0, 0.5))
+    pair = [(reg.dephase, o.dephase), (reg.depolarise, o.depolarise), (reg.damping, o.damping)][k % 3]
+    pair[0](a, p)
+    pair[1](a, p)
+    if k % 5 == 0:
+        reg.h(a)
+        o.apply(O.H, a)
+reg.sync()
+st = qa.capi.getQuESTStats()
+assert st["wavePasses"] > 0 and st["wavePasses"] == st["passes"], st
+err = float(np.max(np.abs(state_of(reg) - o.rho)))
+print("err", err)
+assert err < 2e-6, err
+'''
+
+
+@pytest.mark.gpu
+def test_fp32_density_channels_on_wave_engine_gpu():
+    """fp32 one-qubit channels (CH1 / CHD, packed math on register pairs)
+    and gates on a 10-qubit density matrix on the wave engine, against the
+    NumPy oracle to fp32 precision."""
+    out = _run(["-c", FP32_DENSITY], {"QUEST_PREC": "1", "QUEST_BACKEND": "hip"}, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+
+
 @pytest.mark.gpu
 def test_fp32_wave_matches_fp64_layered_24q_gpu():
     """A 24-qubit random layered circuit on the fp32 wave engine agrees with

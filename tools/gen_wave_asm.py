@@ -67,6 +67,48 @@ PH_KINDS = ["DROT", "DNEG", "DMULI", "DMULNI", "DROTN", "DSC"]   # DSC: real sca
 # depolarising, amplitude damping, density collapse); CHD only scales x1, x2
 CH_KINDS = ["CH1", "CHD"]
 
+# fp32 packed math (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 on registers j,
+# j + 1 held as one 64-bit pair): WAVE_PK=0 keeps scalar fp32 code
+PK = _os.environ.get("WAVE_PK", "1") == "1"
+
+
+def pk_fix(line):
+    """Operand modifiers of a packed fp32 instruction written like its scalar
+    form: v[a:b] pairs pass through (lo -> lo, hi -> hi); S<k> is the op
+    record's coefficient s(76 + k) and B<r> the VGPR r, each broadcast to both
+    halves (op_sel / op_sel_hi pick the dword of the aligned 64-bit pair);
+    inline constants are broadcast; a leading '-' becomes neg_lo / neg_hi."""
+    op, _, rest = line.partition(" ")
+    ops = [x.strip() for x in rest.split(",")]
+    dst, srcs = ops[0], ops[1:]
+    out, sel, selhi, neg = [], [], [], []
+    for x in srcs:
+        n = x.startswith("-")
+        if n:
+            x = x[1:]
+        m = re.fullmatch(r"([SB])(\d+)", x)
+        if m:
+            r = int(m.group(2)) + (76 if m.group(1) == "S" else 0)
+            base, h = r & ~1, r & 1
+            out.append(f"{'s' if m.group(1) == 'S' else 'v'}[{base}:{base + 1}]")
+            sel.append(h)
+            selhi.append(h)
+        elif x.startswith("v["):
+            out.append(x)
+            sel.append(0)
+            selhi.append(1)
+        else:
+            out.append(x)
+            sel.append(0)
+            selhi.append(0)
+        neg.append(1 if n else 0)
+    f = lambda v: "[" + ",".join(map(str, v)) + "]"
+    s = f"{op} {dst}, " + ", ".join(out) + f" op_sel:{f(sel)} op_sel_hi:{f(selhi)}"
+    if any(neg):
+        s += f" neg_lo:{f(neg)} neg_hi:{f(neg)}"
+    return s
+
+
 LAYOUT = {}
 SWAP64 = _os.environ.get("WAVE_SWAP64", "1") == "1"   # register exchanges as 64-bit moves (swap_vals)
 # per-lane selects: v_cmp_*_e64 into this SGPR pair + v_cndmask_b32_e64 (a
@@ -283,13 +325,16 @@ class Gen:
             # 4 temporaries (every set index aliases them: the scheduler keeps
             # the order), the lane-gate coefficients in temporaries 2-3, the
             # lane gates one amplitude at a time: fp64 80 VGPRs, 6 waves per SIMD
-            self.NT = 4
-            self.T = [D + P * (k % 4) for k in range(16)]
-            self.C0, self.C1 = D + 4 * P, D + 5 * P
-            self.vLane, self.vLdB, self.vStB, self.vTmp = D + 6 * P, D + 6 * P + 1, D + 6 * P + 2, D + 6 * P + 3
+            # fp32 with packed math: 8 temporaries (four 64-bit pairs), C0 even
+            nt = 8 if (P == 1 and PK) else 4
+            self.NT = nt
+            self.T = [D + P * (k % nt) for k in range(16)]
+            self.C0, self.C1 = D + nt * P, D + (nt + 1) * P
+            self.vLane, self.vLdB, self.vStB, self.vTmp = (D + (nt + 2) * P, D + (nt + 2) * P + 1,
+                                                           D + (nt + 2) * P + 2, D + (nt + 2) * P + 3)
             self.CL = self.C0             # lane-gate coefficients in C0 / C1 (scratch: vTmp)
             self.CLA = self.C0
-            self.nvgpr = D + 6 * P + 4
+            self.nvgpr = D + (nt + 2) * P + 4
         self.handlers = {}
         # real lane bits below this transpose with a slot through LDS
         # (gen_tr_lds), the others by DPP / v_permlane*_swap
@@ -298,9 +343,14 @@ class Gen:
         self.swap_tmp = 0        # rotating temporary of swap_vals
         self.lane_ctrl = False   # generating a ctrl-2 (lane controls only) handler
         self.buf = None          # straight-line region being collected for scheduling
+        # fp32 packed math: while set, value operands are 64-bit pairs holding
+        # registers j and j + 1 and arithmetic is v_pk_*_f32 (pk_fix)
+        self.packed = False
 
     # ---- helpers --------------------------------------------------------
     def e(self, s):
+        if self.packed and s.startswith("v_pk_"):
+            s = pk_fix(s)
         if self.buf is not None:
             self.buf.append(s)
         else:
@@ -326,13 +376,47 @@ class Gen:
         return self.P * (self.NS + j)
 
     def vp(self, r):
-        return f"v[{r}:{r + 1}]" if self.P == 2 else f"v{r}"
+        return f"v[{r}:{r + 1}]" if (self.P == 2 or self.packed) else f"v{r}"
+
+    def bc(self, r):  # a per-lane value used by every register: broadcast in packed math
+        return f"B{r}" if self.packed else self.vp(r)
 
     def sm(self, k):  # coefficient m[k] in SGPRs (f64 m[8] / f32 m[16] of the op record)
+        if self.packed:
+            return f"S{k}"   # broadcast of s(76 + k), resolved by pk_fix
         return f"s[{76 + 2 * k}:{77 + 2 * k}]" if self.P == 2 else f"s{76 + k}"
 
-    def op(self, name):  # "fma" -> "v_fma_f64" / "v_fma_f32"
+    def op(self, name):  # "fma" -> "v_fma_f64" / "v_fma_f32" (packed: "v_pk_fma_f32")
+        if self.packed:
+            return f"v_pk_{name}_f32"
         return f"v_{name}_{self.F}"
+
+    def mov(self):
+        return "v_mov_b64" if self.packed else self.MOV
+
+    def tmps(self, n, ts):
+        """n temporaries of set ts: packed math takes even-aligned pairs."""
+        if self.packed:
+            return [self.D + 2 * ((ts * n + k) % (self.NT // 2)) for k in range(n)]
+        return [self.T[(n * ts + k) % 16] for k in range(n)]
+
+    def negate(self, r):
+        """Flip the sign of the value at r (packed: of registers r and r + 1)."""
+        if self.packed:
+            self.e(f"v_pk_add_f32 v[{r}:{r + 1}], -v[{r}:{r + 1}], 0")
+        else:
+            self.e(f"v_xor_b32_e32 v{self.hi(r)}, 0x80000000, v{self.hi(r)}")
+
+    def pk_regs(self, js):
+        """Packed math applies to registers j, j + 1 at once: the even j of
+        js when every such pair is in js (else None: scalar code)."""
+        if not (PK and self.P == 1):
+            return None
+        st = set(js)
+        ev = [j for j in js if j % 2 == 0]
+        if len(ev) * 2 != len(js) or any(j + 1 not in st for j in ev):
+            return None
+        return ev
 
     def hi(self, r):     # dword holding the sign bit of the value at r
         return r + self.P - 1
@@ -457,7 +541,7 @@ class Gen:
     # ---- pair math (in place, registers of j and f) ---------------------
     def pair(self, kind, j, f, ts=0):
         r0, i0, r1, i1 = self.vp(self.re(j)), self.vp(self.im(j)), self.vp(self.re(f)), self.vp(self.im(f))
-        T = [self.vp(t) for t in self.T[4 * ts:4 * ts + 4]]
+        T = [self.vp(t) for t in self.tmps(4, ts)]
         m = self.sm
         e = self.e
         # every kind updates the pair in place: products that still need the
@@ -509,8 +593,8 @@ class Gen:
             e(f"{self.op('fma')} {r1}, -{m(3)}, {i0}, {r1}")
             e(f"{self.op('mul')} {i1}, {m(2)}, {i0}")
             e(f"{self.op('fma')} {i1}, {m(3)}, {r0}, {i1}")
-            e(f"{self.MOV} {r0}, {T[0]}")
-            e(f"{self.MOV} {i0}, {T[1]}")
+            e(f"{self.mov()} {r0}, {T[0]}")
+            e(f"{self.mov()} {i0}, {T[1]}")
         elif kind == "SWAP":
             for a, b in ((self.re(j), self.re(f)), (self.im(j), self.im(f))):
                 self.swap_vals(a, b)
@@ -531,7 +615,7 @@ class Gen:
                 self.swap_vals(x, y)
             neg = (self.im(j), self.re(f)) if kind == "YSW" else (self.re(j), self.im(f))
             for r in neg:
-                e(f"v_xor_b32_e32 v{self.hi(r)}, 0x80000000, v{self.hi(r)}")
+                self.negate(r)
         else:
             raise ValueError(kind)
 
@@ -541,6 +625,13 @@ class Gen:
         bench ran 4.5 % faster than with two v_swap_b32 per value
         (WAVE_SWAP64=0 keeps the swaps)."""
         e = self.e
+        if self.packed:   # two fp32 values: 64-bit moves through a temporary pair
+            t = self.D + 2 * (self.swap_tmp % (self.NT // 2))
+            self.swap_tmp += 1
+            e(f"v_mov_b64 v[{t}:{t + 1}], v[{a}:{a + 1}]")
+            e(f"v_mov_b64 v[{a}:{a + 1}], v[{b}:{b + 1}]")
+            e(f"v_mov_b64 v[{b}:{b + 1}], v[{t}:{t + 1}]")
+            return
         if SWAP64 and self.P == 2:
             t = self.T[self.swap_tmp % self.NT]
             self.swap_tmp += 1
@@ -565,7 +656,7 @@ class Gen:
     def cmul_sgpr(self, j, kr, ki, ts=0):
         # (x + iy) *= (m[kr] + i m[ki])
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
-        T = [self.vp(t) for t in self.T[2 * ts:2 * ts + 2]]
+        T = [self.vp(t) for t in self.tmps(2, ts)]
         self.e(f"{self.op('mul')} {T[0]}, {self.sm(ki)}, {y}")
         self.e(f"{self.op('mul')} {T[1]}, {self.sm(ki)}, {x}")
         self.e(f"{self.op('fma')} {x}, {self.sm(kr)}, {x}, -{T[0]}")
@@ -573,11 +664,11 @@ class Gen:
 
     def cmul_vgpr(self, j, cr, ci, ts=0):
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
-        T = [self.vp(t) for t in self.T[2 * ts:2 * ts + 2]]
-        self.e(f"{self.op('mul')} {T[0]}, {self.vp(ci)}, {y}")
-        self.e(f"{self.op('mul')} {T[1]}, {self.vp(ci)}, {x}")
-        self.e(f"{self.op('fma')} {x}, {self.vp(cr)}, {x}, -{T[0]}")
-        self.e(f"{self.op('fma')} {y}, {self.vp(cr)}, {y}, {T[1]}")
+        T = [self.vp(t) for t in self.tmps(2, ts)]
+        self.e(f"{self.op('mul')} {T[0]}, {self.bc(ci)}, {y}")
+        self.e(f"{self.op('mul')} {T[1]}, {self.bc(ci)}, {x}")
+        self.e(f"{self.op('fma')} {x}, {self.bc(cr)}, {x}, -{T[0]}")
+        self.e(f"{self.op('fma')} {y}, {self.bc(cr)}, {y}, {T[1]}")
 
     # ---- handlers --------------------------------------------------------
     def lane_exec_begin(self):
@@ -595,10 +686,17 @@ class Gen:
             self.ctrl_begin()
         else:
             self.region()
+        js = [j for j in range(self.NS) if not (j >> s) & 1]
+        ev = self.pk_regs(js) if (not ctrl and kind != "SWAP") else None
         if self.P == 1 and kind == "SWAP" and not ctrl and SWAP64:
             self.swap_pairs32(s)
+        elif ev:
+            self.packed = True
+            for p, j in enumerate(ev):
+                self.pair(kind, j, j | (1 << s), p % 4)
+            self.packed = False
         else:
-            for p, j in enumerate([j for j in range(self.NS) if not (j >> s) & 1]):
+            for p, j in enumerate(js):
                 f = j | (1 << s)
                 if ctrl:
                     skip = f".Lskip_{kind}_{s}_{j}"
@@ -650,7 +748,15 @@ class Gen:
             self.ctrl_begin()
         else:
             self.region()
-        for p, j in enumerate([j for j in range(self.NS) if not (j >> s) & 1]):
+        js = [j for j in range(self.NS) if not (j >> s) & 1]
+        ev = None if ctrl else self.pk_regs(js)
+        if ev:
+            self.packed = True
+            for p, j in enumerate(ev):
+                self.pair(kind, j, j | (1 << s), p % 4)
+            self.packed = False
+            js = []
+        for p, j in enumerate(js):
             f = j | (1 << s)
             if ctrl:
                 skip = f".Lskip_{kind}_{s}_{j}"
@@ -679,20 +785,25 @@ class Gen:
             e("s_nop 4")
             e("s_mov_b64 exec, s[96:97]")
         self.region()
-        for j in [j for j in range(self.NS) if (j & creg) == creg]:
+        js = [j for j in range(self.NS) if (j & creg) == creg]
+        ev = self.pk_regs(js)
+        if ev:
+            self.packed = True
+            js = ev
+        for j in js:
             x, y = self.re(j), self.im(j)
             if kind in ("DNEG", "DROTN"):
-                e(f"v_xor_b32_e32 v{self.hi(x)}, 0x80000000, v{self.hi(x)}")
-                e(f"v_xor_b32_e32 v{self.hi(y)}, 0x80000000, v{self.hi(y)}")
+                self.negate(x)
+                self.negate(y)
             if kind in ("DROT", "DROTN"):
                 self.rot(x, y, False)
             elif kind in ("DMULI", "DMULNI"):   # x + iy -> -y + ix  /  y - ix
                 self.swap_vals(x, y)
-                r = x if kind == "DMULI" else y
-                e(f"v_xor_b32_e32 v{self.hi(r)}, 0x80000000, v{self.hi(r)}")
+                self.negate(x if kind == "DMULI" else y)
             elif kind == "DSC":   # real factor: two multiplies instead of a complex product
                 e(f"{self.op('mul')} {self.vp(x)}, {self.sm(0)}, {self.vp(x)}")
                 e(f"{self.op('mul')} {self.vp(y)}, {self.sm(0)}, {self.vp(y)}")
+        self.packed = False
         self.end_region()
         if lane:
             e("s_mov_b64 exec, -1")
@@ -703,21 +814,25 @@ class Gen:
         e = self.e
         self.region()
         k = 0
-        for j in range(self.NS):
-            if (j >> a) & 1 or (j >> b) & 1:
-                continue
+        js = [j for j in range(self.NS) if not ((j >> a) & 1 or (j >> b) & 1)]
+        ev = self.pk_regs(js)
+        if ev:
+            self.packed = True
+            js = ev
+        for j in js:
             x = [j, j | (1 << a), j | (1 << b), j | (1 << a) | (1 << b)]
             for base in (self.re, self.im):
                 X = [self.vp(base(r)) for r in x]
                 e(f"{self.op('mul')} {X[1]}, {self.sm(4)}, {X[1]}")
                 e(f"{self.op('mul')} {X[2]}, {self.sm(4)}, {X[2]}")
                 if kind == "CH1":
-                    T = self.vp(self.T[k % 16])
+                    T = self.vp(self.tmps(1, k)[0])
                     k += 1
                     e(f"{self.op('mul')} {T}, {self.sm(2)}, {X[0]}")
                     e(f"{self.op('mul')} {X[0]}, {self.sm(0)}, {X[0]}")
                     e(f"{self.op('fma')} {X[0]}, {self.sm(1)}, {X[3]}, {X[0]}")
                     e(f"{self.op('fma')} {X[3]}, {self.sm(3)}, {X[3]}, {T}")
+        self.packed = False
         self.end_region()
         self.back()
 
@@ -731,7 +846,16 @@ class Gen:
             self.ctrl_begin()
         else:
             self.region()
-        for j in range(self.NS):
+        js = list(range(self.NS))
+        ev = self.pk_regs(js) if (not ctrl and s >= 1) else None
+        if ev:   # registers j, j + 1 share slot bit s >= 1: the same coefficients
+            self.packed = True
+            for j in ev:
+                one = (j >> s) & 1
+                self.cmul_sgpr(j, 2 if one else 0, 3 if one else 1, j % 8)
+            self.packed = False
+            js = []
+        for j in js:
             one = (j >> s) & 1
             if ctrl:
                 skip = f".Lskip_d2s_{s}_{j}"
@@ -764,7 +888,15 @@ class Gen:
             self.ctrl_begin()
         else:
             self.region()
-        for j in range(self.NS):
+        js = list(range(self.NS))
+        ev = None if ctrl else self.pk_regs(js)
+        if ev:
+            self.packed = True
+            for j in ev:
+                self.cmul_vgpr(j, C0, C1, j % 7)
+            self.packed = False
+            js = []
+        for j in js:
             if ctrl:
                 skip = f".Lskip_d2l_{j}"
                 self.ctrl_j(j, skip)
@@ -785,10 +917,13 @@ class Gen:
         self.handler(idx_diag(creg, lane), f"DIAG_m{creg}_l{lane}")
         e = self.e
         js = [j for j in range(self.NS) if (j & creg) == creg]
+        ev = self.pk_regs(js)
         if not lane:
             self.region()
-            for k, j in enumerate(js):
+            self.packed = bool(ev)
+            for k, j in enumerate(ev or js):
                 self.cmul_sgpr(j, 0, 1, k % 8)
+            self.packed = False
             self.end_region()
             self.back()
             return
@@ -808,8 +943,10 @@ class Gen:
             e(f"v_cndmask_b32_e64 v{C0}, 1.0, v{C0}, {SEL}")
             e(f"v_cndmask_b32_e64 v{C1}, 0, v{C1}, {SEL}")
         self.region()
-        for k, j in enumerate(js):
+        self.packed = bool(ev)
+        for k, j in enumerate(ev or js):
             self.cmul_vgpr(j, C0, C1, k % 8)
+        self.packed = False
         self.end_region()
         self.back()
 
@@ -974,8 +1111,8 @@ class Gen:
 
     def lane_math(self, kind, j, px, py, B=None):
         x, y = self.vp(self.re(j)), self.vp(self.im(j))
-        CS, CP = self.vp(self.CL), self.vp(self.CL + self.P)
-        CSr, CSi, CPr, CPi = (self.vp(self.CL + self.P * k) for k in range(4))
+        CS, CP = self.bc(self.CL), self.bc(self.CL + self.P)
+        CSr, CSi, CPr, CPi = (self.bc(self.CL + self.P * k) for k in range(4))
         e = self.e
         px, py = self.vp(px), self.vp(py)
         if kind == "M2R":
@@ -989,7 +1126,7 @@ class Gen:
             e(f"{self.op('fma')} {x}, {CS}, {x}, {py}")
             e(f"{self.op('fma')} {y}, {CS}, {y}, {px}")
         elif kind == "ANTI":
-            CPr, CPi = self.vp(self.CLA), self.vp(self.CLA + self.P)
+            CPr, CPi = self.bc(self.CLA), self.bc(self.CLA + self.P)
             e(f"{self.op('mul')} {x}, {CPr}, {px}")
             e(f"{self.op('mul')} {y}, {CPr}, {py}")
             e(f"{self.op('fma')} {x}, -{CPi}, {py}, {x}")
@@ -1042,6 +1179,21 @@ class Gen:
                         e("s_nop 1")
                         for r, t in zip(regs, tmp):
                             self.lane_fetch(l, r, t)
+            elif PK and self.P == 1 and not ctrl and kind != "M2" and batch == 2:
+                # fp32: the two registers of the batch as one packed pair --
+                # partners fetched into adjacent temporaries, one v_pk op per
+                # two amplitudes (coefficients broadcast)
+                j = js[0]
+                px, py = self.D, self.D + 2
+                for d, r in enumerate((self.re(j), self.re(j) + 1)):
+                    self.lane_fetch(l, px + d, r)
+                for d, r in enumerate((self.im(j), self.im(j) + 1)):
+                    self.lane_fetch(l, py + d, r)
+                self.region()
+                self.packed = True
+                self.lane_math(kind, j, px, py)
+                self.packed = False
+                self.end_region()
             else:
                 slots = []
                 for k, j in enumerate(js):
@@ -1130,6 +1282,7 @@ class Gen:
         vl, vldb, vstb, vt = self.vLane, self.vLdB, self.vStB, self.vTmp
         e("s_load_dwordx4 s[4:7], s[0:1], 0x0")       # re, im
         e("s_load_dwordx2 s[8:9], s[0:1], 0x10")      # launch record
+        e("s_load_dword s100, s[0:1], 0x18")          # tile-index bits to insert (split launches)
         e(f"v_and_b32_e32 v{vl}, 63, v0")
         if self.W:
             # wave index in the workgroup (= its wave bits): lane 0's work-item id / 64
@@ -1331,11 +1484,39 @@ class Gen:
         e(f"s_add_u32 s96, s96, s{bpair}")
         e(f"s_addc_u32 s97, s97, s{bpair + 1}")
 
+    def insert_bits(self, d):
+        """Split launches (a pass run on one part of the state while a qubit
+        swap moves the others, src/hip/backend_hip.hip): kernel argument s100
+        = n (bits 0-1) insertions of bit value v_m (bit 14 + 8m) at tile-index
+        bit j_m (bits 8 + 8m .. 13 + 8m), ascending j -- the launch's tile t
+        becomes the t-th tile whose index has those bits.  n = 0: all tiles."""
+        e = self.e
+        self.ins_label = getattr(self, "ins_label", 0) + 1
+        done = f".Lins_done_{self.ins_label}"
+        e("s_and_b32 s101, s100, 3")
+        for m in range(3):
+            e(f"s_cmp_le_u32 s101, {m}")
+            e(f"s_cbranch_scc1 {done}")
+            e(f"s_bfe_u32 s94, s100, {(6 << 16) | (8 + 8 * m):#x}")      # j
+            e("s_bfm_b64 s[96:97], s94, 0")                               # 2^j - 1
+            e(f"s_and_b64 s[98:99], s[{d}:{d + 1}], s[96:97]")
+            e(f"s_lshr_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s94")
+            e("s_add_u32 s95, s94, 1")
+            e(f"s_lshl_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s95")
+            e(f"s_or_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s[98:99]")
+            e(f"s_bitcmp1_b32 s100, {14 + 8 * m}")                        # v
+            e(f"s_cbranch_scc0 .Lins_zero_{self.ins_label}_{m}")
+            e("s_bfm_b64 s[96:97], 1, s94")
+            e(f"s_or_b64 s[{d}:{d + 1}], s[{d}:{d + 1}], s[96:97]")
+            self.label(f".Lins_zero_{self.ins_label}_{m}")
+        self.label(done)
+
     def base_of(self, tile, d):
         """s[d:d+1] = tile index with zeros inserted at pos[0..K-1] (ascending),
         s[d+2:d+3] = the same in bytes."""
         e = self.e
         e(f"s_mov_b64 s[{d}:{d + 1}], {tile}")
+        self.insert_bits(d)
         K = self.R + 6 + self.W
         assert K <= 24, "pos[] lives in s[20:31] (b >= 12 in bits 8..)"
         for b in range(K):
@@ -1396,7 +1577,7 @@ class Gen:
         L.append("\t.p2align\t6, 0x0")
         L.append("\t.amdhsa_kernel qa_wave_tile")
         lds = self.NW * self.OUTBOX if (self.W or self.tr_lds) else 0
-        for k, v in [("group_segment_fixed_size", lds), ("private_segment_fixed_size", 0), ("kernarg_size", 24),
+        for k, v in [("group_segment_fixed_size", lds), ("private_segment_fixed_size", 0), ("kernarg_size", 32),
                      ("user_sgpr_count", 2), ("user_sgpr_dispatch_ptr", 0), ("user_sgpr_queue_ptr", 0),
                      ("user_sgpr_kernarg_segment_ptr", 1), ("user_sgpr_dispatch_id", 0),
                      ("user_sgpr_kernarg_preload_length", 0), ("user_sgpr_kernarg_preload_offset", 0),
@@ -1404,7 +1585,7 @@ class Gen:
                      ("enable_private_segment", 0), ("system_sgpr_workgroup_id_x", 1),
                      ("system_sgpr_workgroup_id_y", 0), ("system_sgpr_workgroup_id_z", 0),
                      ("system_sgpr_workgroup_info", 0), ("system_vgpr_workitem_id", 0),
-                     ("next_free_vgpr", nv8), ("next_free_sgpr", 100), ("accum_offset", nv8),
+                     ("next_free_vgpr", nv8), ("next_free_sgpr", 102), ("accum_offset", nv8),
                      ("reserve_vcc", 1), ("float_round_mode_32", 0), ("float_round_mode_16_64", 0),
                      ("float_denorm_mode_32", 3), ("float_denorm_mode_16_64", 3), ("dx10_clamp", 1),
                      ("ieee_mode", 1), ("fp16_overflow", 0), ("tg_split", 0)]:
@@ -1430,9 +1611,12 @@ amdhsa.kernels:
         .offset:         16
         .size:           8
         .value_kind:     global_buffer
+      - .offset:         24
+        .size:           4
+        .value_kind:     by_value
     .group_segment_fixed_size: {lds}
     .kernarg_segment_align: 8
-    .kernarg_segment_size: 24
+    .kernarg_segment_size: 32
     .language:       OpenCL C
     .language_version:
       - 2
@@ -1440,7 +1624,7 @@ amdhsa.kernels:
     .max_flat_workgroup_size: {64 * self.NW}
     .name:           qa_wave_tile
     .private_segment_fixed_size: 0
-    .sgpr_count:     102
+    .sgpr_count:     104
     .sgpr_spill_count: 0
     .symbol:         qa_wave_tile.kd
     .uniform_work_group_size: 1
