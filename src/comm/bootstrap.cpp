@@ -172,8 +172,21 @@ void allgather(int rank, int size, const void* mine, void* all, size_t bytes) {
                 close(fd);   // a connection its rank abandoned; the rank retries
                 continue;
             }
-            if (r <= 0 || r >= size || fds[r] >= 0) fatal("bad rank in bootstrap");
-            readAll(fd, out + (size_t)r * bytes, bytes);
+            if (r <= 0 || r >= size) {   // not one of ours (another job on a reused port)
+                close(fd);
+                continue;
+            }
+            if (!tryReadAll(fd, out + (size_t)r * bytes, bytes)) {
+                close(fd);
+                continue;
+            }
+            if (fds[r] >= 0) {
+                // the rank gave up on an earlier connection (greeting timeout)
+                // after rank 0 had accepted it: keep the newest
+                close(fds[r]);
+                fds[r] = fd;
+                continue;
+            }
             fds[r] = fd;
             k++;
         }
