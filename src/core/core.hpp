@@ -103,6 +103,10 @@ struct QuregImpl {
     // local positions the planner keeps out of tile padding (router planSwap:
     // the victims of the swap being prepared; 0 otherwise)
     u64 tileAvoid = 0;
+    // logical qubits a swap about to run moves out (router planSwap, before
+    // its flush; -1 none): the backend can split the passes that avoid them
+    int swapVictims[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    int nSwapVictims = 0;
     bool permIdentity() const {
         for (int i = 0; i < nSV; i++)
             if (l2p[i] != i) return false;

@@ -485,7 +485,19 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
             if (!comm::swapsInPlace() && comm::exchangeStreamOrdered()) be::preSwap(q, ls, k, myG);
         }
     }
+    if (k == 0) {   // the victims as logical qubits (the same choice after the flush)
+        int g2[8], l2[8];
+        const int k2 = chooseVictims(q, lq, 0, g2, l2);
+        q.nSwapVictims = k2;
+        for (int m = 0; m < k2; m++) q.swapVictims[m] = q.p2l[l2[m]];
+        // (their positions stay out of tile padding: a pass that does not
+        // target them leaves them out)
+        static const bool avoidPad = !getenv("QUEST_SWAP_AVOID") || atoi(getenv("QUEST_SWAP_AVOID")) != 0;
+        if (avoidPad)
+            for (int m = 0; m < k2; m++) q.tileAvoid |= 1ull << l2[m];
+    }
     be::flush(q);
+    q.nSwapVictims = 0;
     if (k == 0) k = chooseVictims(q, lq, 0, gp, lp);
     if (k == 0) {
         fprintf(stderr, "QuEST: no local qubit available for a distributed swap\n");

@@ -360,6 +360,35 @@ bool relabelsLower(const TileProgram& prog) {
 }
 
 long long g_waveStoreTrCost = 0;
+
+// QUEST_CNOT_STATS=1 (planner study): why deferred CNOTs were executed, by
+// reason and by the domains of control / target -- printed at exit
+namespace {
+const char* kCnotReason[] = {"ctrl-of-deferred-has-conds", "target-conditions-others", "channel", "op-control-has-conds",
+                             "phase-mask-has-conds", "gate-on-control", "gate-on-target", "diag-run", "end-of-pass"};
+long long g_cnotStats[9][3][3];
+bool cnotStatsOn() {
+    static const bool on = getenv("QUEST_CNOT_STATS") != nullptr;
+    return on;
+}
+struct CnotStatsPrinter {
+    ~CnotStatsPrinter() {
+        if (!cnotStatsOn()) return;
+        const char* dn[] = {"slot", "lane", "wave"};
+        long long tot = 0;
+        for (auto& a : g_cnotStats)
+            for (auto& b : a)
+                for (long long v : b) tot += v;
+        fprintf(stderr, "executed deferred CNOTs: %lld\n", tot);
+        for (int r = 0; r < 9; r++)
+            for (int c = 0; c < 3; c++)
+                for (int t = 0; t < 3; t++)
+                    if (g_cnotStats[r][c][t])
+                        fprintf(stderr, "  %-28s control %-4s target %-4s %6lld (%.1f %%)\n", kCnotReason[r], dn[c], dn[t],
+                                g_cnotStats[r][c][t], 100.0 * g_cnotStats[r][c][t] / tot);
+    }
+} g_cnotStatsPrinter;
+}  // namespace
 thread_local int t_planQuiet = 0;
 thread_local int t_waveCframe = -1;
 
@@ -1167,9 +1196,14 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         return m;
     };
     // ops in physical terms (no frame adjustment): a CNOT c -> t, a Z, a CZ
+    int cnotReason = 0;
     auto rawCnot = [&](int i, int c, int t) {
         WaveOp x;
         const int wt = lay.where[t];
+        if (cnotStatsOn() && !t_planQuiet) {
+            auto dom = [&](int w) { return inSlot(w) ? 0 : laneOf(w) < kWaveLanes ? 1 : 2; };
+            g_cnotStats[cnotReason][dom(lay.where[c])][dom(wt)]++;
+        }
         if (!inSlot(wt) && laneOf(wt) < kWaveLaneOps) {
             x = blank((int)WKind::LSWAP);
             x.a = laneOf(wt);
@@ -1210,19 +1244,23 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         postClear = false;
         if (deferCnot(i)) {
             const int t = op.t[0], k = __builtin_ctz(op.ctrlIn);
+            cnotReason = 0;
             if (Cnd[k]) execConds(i, k);   // the control must be a plain physical bit
+            cnotReason = 1;
             if (deps(t)) clean(i, t);       // the target must not condition other bits
             Cnd[t] ^= 1u << k;
             F ^= ((F >> k) & 1u) << t;     // x_t ^= x_k = p_k ^ F_k
             return 1;
         }
         if (chan[i]) {
+            cnotReason = 2;
             for (int b : {op.t[0], op.t[1]}) {
                 execConds(i, b);
                 clean(i, b);
             }
             return 0;
         }
+        cnotReason = 3;
         for (unsigned m = op.ctrlIn; m; m &= m - 1)
             if (Cnd[__builtin_ctz(m)]) execConds(i, __builtin_ctz(m));
         const real* m = op.m;
@@ -1241,6 +1279,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
                 if ((F >> zt) & 1u) sig.mul(-1, 0);
                 return 1;
             }
+            cnotReason = 4;
             for (unsigned b = mask; b; b &= b - 1)
                 if (Cnd[__builtin_ctz(b)]) execConds(i, __builtin_ctz(b));
             return 0;
@@ -1249,6 +1288,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
         const bool unc = op.ctrlIn == 0 && op.ctrlOut == 0;
         const bool isY = cls[i] == M2Class::Anti && m[2] == 0 && m[4] == 0 && std::fabs(m[3]) == 1 && m[5] == -m[3];
         // an uncontrolled X / Y on a condition only toggles F_t (and a Z on p_t)
+        cnotReason = 5;
         if (deps(t) && !(unc && t >= VB && (cls[i] == M2Class::Swap || isY))) clean(i, t);
         if (!Cnd[t] || cls[i] == M2Class::Swap) return 0;   // X commutes with the orientation
         const bool commX = near(m[0], m[6]) && near(m[1], m[7]) && near(m[2], m[4]) && near(m[3], m[5]);
@@ -1276,6 +1316,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             postClear = true;
             return 0;
         }
+        cnotReason = 6;
         execConds(i, t);
         return 0;
     };
@@ -1331,7 +1372,10 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             if (j - i >= 2) {
                 for (int x = i; x < j; x++)
                     for (unsigned b = ops[x].ctrlIn; b; b &= b - 1)
-                        if (cframeOn && Cnd[__builtin_ctz(b)]) execConds(x, __builtin_ctz(b));
+                        if (cframeOn && Cnd[__builtin_ctz(b)]) {
+                            cnotReason = 7;
+                            execConds(x, __builtin_ctz(b));
+                        }
                 std::vector<unsigned> masksIn;
                 for (int x = i; x < j; x++)
                     if (std::find(masksIn.begin(), masksIn.end(), ops[x].ctrlIn) == masksIn.end())
@@ -1623,6 +1667,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             if (!ok) bad = t;
         }
         if (bad < 0) break;
+        cnotReason = 8;
         execConds(nOps, bad);
     }
     if (!storeLayout(lay, true)) return false;

@@ -556,6 +556,34 @@ void flushImpl(QuregImpl& q, bool front) {
     // QUEST_PLAN_ONLY=1 (planner studies): plan, count, do not touch the
     // state -- pass counts of large registers in no time (tools/plan_study.py)
     static const bool planOnly = getenv("QUEST_PLAN_ONLY") && atoi(getenv("QUEST_PLAN_ONLY")) != 0;
+    // QUEST_SWAP_STUDY=1: the passes of a pre-swap flush after the last one
+    // whose tile holds a victim of the swap (they could run split around it)
+    static const bool swapStudy = getenv("QUEST_SWAP_STUDY") != nullptr;
+    if (swapStudy && q.nSwapVictims > 0 && rt().rank == 0) {
+        int cur[8];
+        for (int m = 0; m < q.nSwapVictims; m++) cur[m] = q.l2p[q.swapVictims[m]];
+        int last = -1;
+        double opsAfter = 0, opsAll = 0;
+        for (size_t p = 0; p < prog.passes.size(); p++) {
+            const TilePass& ps = prog.passes[p];
+            bool in = false;
+            for (int m = 0; m < q.nSwapVictims; m++)
+                for (int b = 0; b < ps.k; b++)
+                    if (ps.pos[b] == cur[m]) {
+                        in = true;
+                        cur[m] = ps.stPos[b];
+                        break;
+                    }
+            if (in) last = (int)p;
+        }
+        for (size_t p = 0; p < prog.passes.size(); p++) {
+            const double n = prog.passes[p].opEnd - prog.passes[p].opBegin;
+            opsAll += n;
+            if ((int)p > last) opsAfter += n;
+        }
+        fprintf(stderr, "swap study: %zu passes before the swap, %zu after the last holding a victim (%.0f of %.0f ops)\n",
+                prog.passes.size(), prog.passes.size() - (size_t)(last + 1), opsAfter, opsAll);
+    }
     if (planOnly) {
         for (const TilePass& ps : prog.passes) {
             WaveProgram wp;
