@@ -387,6 +387,8 @@ void fuseGates(std::vector<Op>& ops) {
     ops.swap(out);
 }
 
+thread_local int t_planCommute = -1;
+
 bool programRelabels(const TileProgram& prog) {
     for (const TilePass& ps : prog.passes)
         for (int i = 0; i < ps.k; i++)
@@ -523,7 +525,7 @@ int& diagAsPhases() {
 // -4 .. +4): more freedom per pass does not make the greedy plan better.
 bool planCommute() {
     static const bool v = getenv("QUEST_PLAN_COMMUTE") && atoi(getenv("QUEST_PLAN_COMMUTE")) != 0;
-    return v;
+    return t_planCommute >= 0 ? t_planCommute != 0 : v;
 }
 
 // 0: diagonal 2x2, 1: a I + b X, 2: anything else (multi-target ops too)

@@ -190,6 +190,10 @@ struct PlanHooks {
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,
                const PlanHooks* hooks = nullptr);
+// class-aware commutation in the pass scheduler for this thread's plans
+// (-1: QUEST_PLAN_COMMUTE, default off; 0 off; 1 on) -- a strategy of the
+// wave planner's search (searchWaveStrategy)
+extern thread_local int t_planCommute;
 // Whether any pass of the program stores with a permuted layout.
 bool programRelabels(const TileProgram& prog);
 

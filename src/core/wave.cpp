@@ -492,13 +492,16 @@ struct WaveStrategy {
     int seeds;     // seed candidates per pass (0: default)
     double look;   // one-pass lookahead weight (< 0: default)
     int cframe;    // conditional exchange frame: 1 as configured, 0 off
+    int commute;   // class-aware commutation in the scheduler (t_planCommute): -1 as configured, 0 off, 1 on
 };
 // 0 is the configured default (cost = -1, cframe = -1: waveCostHooks and the
-// environment as they are); the last one is the round-3 planner (no
-// compute-aware passes, no conditional frame)
-const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1}, {1, 1, 0, -1, 1}, {0, 0, 0, -1, 1}, {1, 0, 0, -1, 1},
-                                    {0, 2, 0, -1, 1},  {0, 1, 48, -1, 1}, {0, 1, 0, 0.5, 1}, {0, 0, 0, -1, 0},
-                                    {-1, 1, 0, -1, 1}, {-1, 0, 0, -1, 1}};
+// environment as they are); the 8th is the round-3 planner (no compute-aware
+// passes, no conditional frame); then class-aware commutation variants
+const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1, -1}, {1, 1, 0, -1, 1, -1}, {0, 0, 0, -1, 1, -1},
+                                    {1, 0, 0, -1, 1, -1},   {0, 2, 0, -1, 1, -1},  {0, 1, 48, -1, 1, -1},
+                                    {0, 1, 0, 0.5, 1, -1},  {0, 0, 0, -1, 0, -1},  {0, -1, 0, -1, -1, 1},
+                                    {1, 1, 0, -1, 1, 1},    {0, 0, 0, -1, 1, 1},   {1, 0, 0, -1, 1, 1},
+                                    {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1}};
 constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
 // strategies the search tries (QUEST_PLAN_STRATEGIES, default 8: the last two,
 // one fewer resident low position, are opt-in)
@@ -584,6 +587,7 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
         QuietPlan quiet;
         fuseBlockQubits() = fuse;              // (thread-local)
         t_waveCframe = kStrategies[i].cframe;  // (thread-local)
+        t_planCommute = kStrategies[i].commute;
         const int c = cdefault + kStrategies[i].dc;
         score[i] = 1e300;
         if (c < kWaveBits - 1) {
@@ -602,6 +606,7 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
             score[i] = t;
         }
         t_waveCframe = -1;
+        t_planCommute = -1;
         took[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tRun0).count();
     };
     std::vector<std::thread> pool;
@@ -629,11 +634,15 @@ WaveStrategyScope::WaveStrategyScope(int idx, int cdefault, PlanHooks& hooks, in
     *cmin = cdefault + kStrategies[idx].dc;
     strategyHooks(kStrategies[idx], hooks);
     t_waveCframe = kStrategies[idx].cframe;
+    t_planCommute = kStrategies[idx].commute;
     active = true;
 }
 
 WaveStrategyScope::~WaveStrategyScope() {
-    if (active) t_waveCframe = -1;
+    if (active) {
+        t_waveCframe = -1;
+        t_planCommute = -1;
+    }
 }
 
 int chooseWaveCmin(QuregImpl& q, int cdefault, const PlanHooks& hooks) {
