@@ -467,22 +467,25 @@ n = int(sys.argv[2])
 r = qa.Register(env, n)
 r.init_plus()
 capi.resetQuESTStats()
-random_layered(n, 12, seed=3).apply(r)
-r.sync()
-p = [r.prob(q, 1) for q in (0, n - 1)]
-# a window whose passes after the swap leave the incoming qubit out of their
-# tiles (it only controls them): the split launches run next to the transfer
-top = n - 1
+# a window whose ops before the swap leave local qubit hi alone and whose ops
+# after it use hi last: hi is the victim, chosen before the pre-swap flush;
+# the passes of that flush leave its position out of their tiles, so they run
+# on the parts the swap sends first and on the part it keeps next to the transfer
+top, hi = n - 1, 20
 rng = np.random.default_rng(4)
-r.h(top)
-for q in range(top):
-    r.cnot(top, q)
-for layer in range(10):
-    for q in range(top):
+for layer in range(6):
+    for q in range(hi):
         r.ry(q, float(rng.uniform(0, 3)))
-    for q in range(layer % 2, top - 1, 2):
+    for q in range(layer % 2, hi - 1, 2):
         r.cnot(q, q + 1)
-    r.crz(top, layer % top, 0.3)
+r.h(top)
+for q in range(hi + 1):
+    r.cnot(top, q)
+r.sync()
+p = [r.prob(q, 1) for q in (0, hi, top)]
+# a random layered circuit: its passes next to a swap always hold a swapped
+# position (no split)
+random_layered(n, 12, seed=3).apply(r)
 r.sync()
 st = capi.getQuESTStats()
 v = r.to_numpy()
@@ -496,12 +499,11 @@ if env.rank == 0:
 def test_overlapped_swaps_rccl_shared_gpu(genv, tmp_path, ranks):
     """Overlapped swaps (QUEST_SWAP_OVERLAP, default on): RCCL ranks sharing
     the GPU (QUEST_RCCL_SHARED_GPU=1, the RCCL path of a multi-GPU node) with
-    21 local qubits.  A random layered circuit (whose passes next to a swap
-    always hold a swapped position: no split), then a window whose passes
-    after the swap only use the incoming qubit as a control: they start on
-    the part of the chunk the swap leaves in place while the exchange runs
-    on its own stream.  The state equals the single-rank run's and the split
-    launches really happened."""
+    21 local qubits.  A window whose ops before the swap leave the victim
+    alone (its passes split: the parts the swap sends first, the kept part
+    next to the transfer), then a random layered circuit (whose passes next to
+    a swap always hold a swapped position: no split).  The state equals the
+    single-rank run's and the split launches really happened."""
     from quest_amd.parallel import spawn_local
 
     here = os.path.dirname(os.path.abspath(__file__))
