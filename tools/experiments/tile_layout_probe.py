@@ -37,6 +37,7 @@ def main():
         "r4 p7 7,8,10,18-20": [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 18, 19, 20],
         "r4 p18 7,10,13,19,22,24": [0, 1, 2, 3, 4, 5, 6, 7, 10, 13, 19, 22, 24],
         "contiguous 0-12": list(range(13)),
+        "unfused H 15 (direct)": [15],
         "0-3 + 4-12 (same)": list(range(13)),
         "0-3 + every 3rd": [0, 1, 2, 3, 7, 10, 13, 16, 19, 22, 25, 27, 29],
         "0-3 + top 9": [0, 1, 2, 3] + list(range(n - 9, n)),
