@@ -503,12 +503,15 @@ const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1, -1}, {1, 1, 0, -1, 1, -1}
                                     {1, 1, 0, -1, 1, 1},    {0, 0, 0, -1, 1, 1},   {1, 0, 0, -1, 1, 1},
                                     {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1}};
 constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
-// strategies the search tries (QUEST_PLAN_STRATEGIES, default 8: the last two,
-// one fewer resident low position, are opt-in)
+// strategies the search tries (QUEST_PLAN_STRATEGIES, default all 14: with
+// the commutation and one-fewer-resident-position variants the five bench
+// seeds plan 80 passes instead of 82, 0.1306 vs 0.1317 ms / gate over three
+// interleaved rounds on one box, profiles/r5/search_strategies_ab.txt; 11
+// circuit seeds 177 instead of 183 passes in the host model)
 int searchStrategies() {
     static const int n = [] {
         const char* e = getenv("QUEST_PLAN_STRATEGIES");
-        const int v = e ? atoi(e) : 8;
+        const int v = e ? atoi(e) : kNumStrategies;
         return v < 1 ? 1 : v > kNumStrategies ? kNumStrategies : v;
     }();
     return n;
