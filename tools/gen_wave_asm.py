@@ -1511,11 +1511,43 @@ class Gen:
             self.label(f".Lins_zero_{self.ins_label}_{m}")
         self.label(done)
 
+    def tile_order(self, d):
+        """Experiment (QUEST_WAVE_TILE_ORDER, bits 2-3 of the launch argument
+        s100): the order in which the launch's tiles are dealt to workgroups.
+        0: tile = index; 1: bit-reversed index (workgroups running together
+        differ in the HIGH non-tile positions); 2: XCD blocks (index i takes
+        tile (i % 8) * T / 8 + i / 8: the workgroups an XCD runs together take
+        adjacent tiles of its own eighth).  T = the launch's tile count (a power
+        of two, >= 8, else the order stays 0)."""
+        e = self.e
+        self.ord_label = getattr(self, "ord_label", 0) + 1
+        done, blk = f".Lord_done_{self.ord_label}", f".Lord_blk_{self.ord_label}"
+        e("s_bfe_u32 s94, s100, 0x20002")             # order (bits 2-3)
+        e("s_cmp_eq_u32 s94, 0")
+        e(f"s_cbranch_scc1 {done}")
+        e("s_ff1_i32_b32 s95, s12")                   # log2 T
+        e("s_cmp_lt_u32 s95, 3")
+        e(f"s_cbranch_scc1 {done}")
+        e("s_cmp_eq_u32 s94, 1")
+        e(f"s_cbranch_scc0 {blk}")
+        e(f"s_brev_b32 s{d}, s{d}")
+        e("s_sub_u32 s94, 32, s95")
+        e(f"s_lshr_b32 s{d}, s{d}, s94")
+        e(f"s_branch {done}")
+        self.label(blk)
+        e(f"s_and_b32 s94, s{d}, 7")
+        e("s_sub_u32 s98, s95, 3")
+        e("s_lshl_b32 s94, s94, s98")
+        e(f"s_lshr_b32 s{d}, s{d}, 3")
+        e(f"s_or_b32 s{d}, s{d}, s94")
+        self.label(done)
+
     def base_of(self, tile, d):
         """s[d:d+1] = tile index with zeros inserted at pos[0..K-1] (ascending),
         s[d+2:d+3] = the same in bytes."""
         e = self.e
         e(f"s_mov_b64 s[{d}:{d + 1}], {tile}")
+        self.tile_order(d)
         self.insert_bits(d)
         K = self.R + 6 + self.W
         assert K <= 24, "pos[] lives in s[20:31] (b >= 12 in bits 8..)"
