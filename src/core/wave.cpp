@@ -13,6 +13,7 @@
 
 namespace qa {
 
+extern thread_local int t_planQuiet;
 namespace {
 
 constexpr int kInf = 1 << 30;
@@ -137,6 +138,130 @@ void phaseOf(const WaveOp& w, double* pr, double* pi) {
             *pi = sn;
         }
     }
+}
+
+// Sign frame (round 5, QUEST_WAVE_ZFRAME=0 to disable): a Z on one register
+// location -- a slot, a real lane bit or a wave bit, the DNEG ops a pass emits
+// for Z / S^2-like gates and for the conditional frame's bookkeeping, 8 % of
+// the bench passes' VALU instructions -- is not executed where it stands but
+// carried along the pass's ops in a set of pending locations and applied once
+// at the end (usually cancelled or absorbed first):
+//   * diagonal ops and ops controlled by the location commute with it;
+//   * a transposition moves it with the bit (TR swaps two locations);
+//   * a 2x2 op on the location is conjugated instead, U Z = Z (Z U Z): the
+//     off-diagonal entries of its matrix change sign (general, real, Rx-form,
+//     anti-diagonal kinds on slots and lanes), a rotation's angle too, Y <-> -Y;
+//   * an X / CNOT on it (SWAP, LSWAP) with one plain control c: CX Z_t =
+//     Z_t Z_c CX, the op stays and c joins the pending set;
+//   * an uncontrolled X (X Z = -Z X: a global sign with nowhere to go here),
+//     a multi-controlled X, an unnormalised Hadamard and channels apply the
+//     pending Z first.
+// Emulated and GPU passes run the transformed list, so the host emulation
+// (QUEST_CPU_PLANNER=3) checks it against the oracle like any other plan.
+void zFrame(WaveProgram& out, size_t begin) {
+    static const bool on = !getenv("QUEST_WAVE_ZFRAME") || atoi(getenv("QUEST_WAVE_ZFRAME")) != 0;
+    if (!on || out.ops.size() <= begin) return;
+    constexpr int nLoc = kWaveSlots + kWaveLaneBits;   // slots, then lane / wave bits
+    bool z[nLoc] = {false};
+    auto zOp = [](int loc) {
+        WaveOp w;
+        memset(&w, 0, sizeof w);
+        w.kind = (int)WKind::DNEG;
+        if (loc < kWaveSlots)
+            w.cReg = 1u << loc;
+        else
+            w.cLane = 1u << (loc - kWaveSlots);
+        return w;
+    };
+    std::vector<WaveOp> res(out.ops.begin(), out.ops.begin() + (long)begin);
+    static long long why[4];   // QUEST_ZFRAME_STATS: HADD, X, channel, end
+    static const bool zst = getenv("QUEST_ZFRAME_STATS") != nullptr;
+    static struct P { ~P() { if (zst) fprintf(stderr, "zframe flushes: H %lld X %lld chan %lld end %lld\n", why[0], why[1], why[2], why[3]); } } printer;
+    int reason = 3;
+    auto flush = [&](int loc) {
+        if (loc >= 0 && loc < nLoc && z[loc]) {
+            res.push_back(zOp(loc));
+            z[loc] = false;
+            if (!t_planQuiet) why[reason]++;
+        }
+    };
+    auto single = [](const WaveOp& w, int* loc) {   // one plain control location, nothing else
+        if (w.ctrlOut || w.ctrlOutZero || w.cLaneZero || (w.cReg & w.fReg) || (w.cLane & w.fLane)) return false;
+        const int n = __builtin_popcount(w.cReg) + __builtin_popcount(w.cLane);
+        if (n != 1) return false;
+        *loc = w.cReg ? __builtin_ctz(w.cReg) : kWaveSlots + __builtin_ctz(w.cLane);
+        return true;
+    };
+    for (size_t o = begin; o < out.ops.size(); o++) {
+        WaveOp w = out.ops[o];
+        const WKind k = (WKind)w.kind;
+        int loc = -1;
+        if (k == WKind::DNEG && single(w, &loc)) {
+            z[loc] = !z[loc];
+            continue;
+        }
+        if (k == WKind::TR) {
+            std::swap(z[w.a], z[kWaveSlots + w.b]);
+            res.push_back(w);
+            continue;
+        }
+        const bool slotTarget = k == WKind::M2 || k == WKind::M2R || k == WKind::M2RI || k == WKind::ANTI ||
+                                k == WKind::SWAP || k == WKind::ROTY || k == WKind::ROTX || k == WKind::HADD ||
+                                k == WKind::YSW || k == WKind::YSWC;
+        const bool laneTarget = k == WKind::LM2R || k == WKind::LM2RI || k == WKind::LANTI || k == WKind::LSWAP;
+        if (k == WKind::CH1 || k == WKind::CHD) {
+            reason = 2;
+            flush(w.a);
+            flush(w.b);
+            res.push_back(w);
+            continue;
+        }
+        if (!slotTarget && !laneTarget) {   // diagonal kinds: commute
+            res.push_back(w);
+            continue;
+        }
+        const int t = slotTarget ? w.a : kWaveSlots + w.a;
+        if (!z[t]) {
+            res.push_back(w);
+            continue;
+        }
+        switch (k) {
+            case WKind::M2:   // (re, im) pairs: u00, u01, u10, u11
+                for (int i = 2; i < 6; i++) w.m[i] = -w.m[i];
+                break;
+            case WKind::M2R: case WKind::M2RI: case WKind::LM2R: case WKind::LM2RI:
+                w.m[1] = -w.m[1];
+                w.m[2] = -w.m[2];
+                break;
+            case WKind::ANTI: case WKind::LANTI:
+                for (int i = 0; i < 4; i++) w.m[i] = -w.m[i];
+                break;
+            case WKind::ROTY: case WKind::ROTX:
+                w.m[0] = -w.m[0];
+                w.m[1] = -w.m[1];
+                break;
+            case WKind::YSW: w.kind = (int)WKind::YSWC; break;
+            case WKind::YSWC: w.kind = (int)WKind::YSW; break;
+            case WKind::SWAP: case WKind::LSWAP: {
+                int c = -1;
+                if (single(w, &c)) {
+                    z[c] = !z[c];
+                } else {
+                    reason = 1;
+                    flush(t);
+                }
+                break;
+            }
+            default:   // HADD
+                reason = 0;
+                flush(t);
+                break;
+        }
+        res.push_back(w);
+    }
+    reason = 3;
+    for (int loc = 0; loc < nLoc; loc++) flush(loc);
+    out.ops.swap(res);
 }
 
 // Merge the phase ops of every run of consecutive diagonal ops in
@@ -1702,6 +1827,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     wp.stFlipLane = laneFlips();
     for (int s = 0; s < kWaveSlots; s++) wp.stSlot[s] = lay.slotBit[s];
     for (int l = 0; l < kWaveLaneBits; l++) wp.stLane[l] = lay.laneBit[l];
+    zFrame(out, (size_t)wp.opBegin);
     wp.opEnd = (int)out.ops.size();
     for (int o = wp.opBegin; o < wp.opEnd; o++)
         wp.waveExchange = wp.waveExchange || (out.ops[(size_t)o].kind == (int)WKind::TR && out.ops[(size_t)o].b >= kWaveLanes);
