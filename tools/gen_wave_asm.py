@@ -111,6 +111,16 @@ def pk_fix(line):
 
 LAYOUT = {}
 SWAP64 = _os.environ.get("WAVE_SWAP64", "1") == "1"   # register exchanges as 64-bit moves (swap_vals)
+# X / CNOT on lane bit 2 (LSWAP) through the LDS crossbar: one ds_swizzle_b32
+# per dword (lane ^ 4) instead of two bank-masked DPP moves plus a 64-bit copy
+# per value -- 320 VALU instructions per handler moved off the VALU, which the
+# op-heavy passes are bound by (tools/experiments/valu_rate.hip: ds_swizzle
+# issues at 1.5x an fp64 op per SIMD on the LDS pipe).  WAVE_SWZ=2: lane bits
+# 0 and 1 too (their DPP version is 128 VALU; bench 0.1277 vs 0.1279 with
+# lane bit 2 only vs 0.1289 ms/gate without, three rounds on one box), 3: the
+# partner fetches of the lane-bit gates (LM2R / LM2RI / LANTI) as well, 0: DPP
+# only.
+SWZ = int(_os.environ.get("WAVE_SWZ", "2"))
 # per-lane selects: v_cmp_*_e64 into this SGPR pair + v_cndmask_b32_e64 (a
 # v_cndmask_b32_e32 reading vcc issues ~5x slower on gfx950, tools/isa_micro.hip)
 SEL = "s[98:99]"
@@ -1067,7 +1077,11 @@ class Gen:
 
     # ---- gates on lane bits 0-3 (no transposition) --------------------
     def lane_fetch(self, l, dst, src):
-        """dst dword <- the partner lane's (lane ^ 2^l) src dword."""
+        """dst dword <- the partner lane's (lane ^ 2^l) src dword (WAVE_SWZ >= 3:
+        through the LDS crossbar, the caller waits for lgkmcnt before use)."""
+        if SWZ >= 3 and l <= 2:
+            self.e(f"ds_swizzle_b32 v{dst}, v{src} offset:{0x1f | ((1 << l) << 10):#x}")
+            return
         if l < 2:
             qp = "[1,0,3,2]" if l == 0 else "[2,3,0,1]"
             self.e(f"v_mov_b32_dpp v{dst}, v{src} quad_perm:{qp} row_mask:0xf bank_mask:0xf")
@@ -1165,7 +1179,13 @@ class Gen:
             if kind == "SWAP":
                 for j in js:
                     regs = [self.re(j) + d for d in range(self.P)] + [self.im(j) + d for d in range(self.P)]
-                    if l < 2:
+                    if (l == 2 and SWZ >= 1) or (l < 2 and SWZ >= 2):
+                        # in place: every lane's dword is read at issue (the
+                        # partner lane ^ 2^l is active whenever this one is:
+                        # a lane control is never the target bit)
+                        for r in regs:
+                            e(f"ds_swizzle_b32 v{r}, v{r} offset:{0x1f | ((1 << l) << 10):#x}")
+                    elif l < 2:
                         for r in regs:   # in place: DPP reads every lane before writing
                             self.lane_fetch(l, r, r)
                     else:
@@ -1189,6 +1209,8 @@ class Gen:
                     self.lane_fetch(l, px + d, r)
                 for d, r in enumerate((self.im(j), self.im(j) + 1)):
                     self.lane_fetch(l, py + d, r)
+                if SWZ >= 3 and l <= 2:
+                    e("s_waitcnt lgkmcnt(0)")
                 self.region()
                 self.packed = True
                 self.lane_math(kind, j, px, py)
@@ -1203,6 +1225,8 @@ class Gen:
                         self.lane_fetch(l, px + d, self.re(j) + d)
                         self.lane_fetch(l, py + d, self.im(j) + d)
                     slots.append((j, px, py, B))
+                if SWZ >= 3 and l <= 2:
+                    e("s_waitcnt lgkmcnt(0)")
                 if not ctrl:
                     self.region()
                 for j, px, py, B in slots:
@@ -1213,7 +1237,7 @@ class Gen:
                 self.label(skip)
         if ctrl:
             self.ctrl_end()
-        self.back()
+        self.back()   # (next_op waits for lgkmcnt(0): the swizzles have landed)
 
     def gen_trw(self, s, b):
         """Transpose slot s with wave bit b through LDS: the wave with the bit
