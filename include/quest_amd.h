@@ -147,6 +147,7 @@ typedef struct QuESTStats {
     long long swapMicros;     /* device time of the qubit swaps (HIP: events on the compute stream; reading waits for them) */
     long long overlappedSwaps;  /* swaps run on a stream of their own, next to gate passes (QUEST_SWAP_OVERLAP) */
     long long overlappedPasses; /* passes started on the part of the chunk a swap in flight leaves in place */
+    long long layoutAligns;   /* swaps / chunk restores before which this rank moved its local qubits to rank 0's positions */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

@@ -82,7 +82,8 @@ class _Binding:
                         ("opsQueued", "passes", "fusedOps", "swaps", "bytesExchanged", "reductions",
                          "verifiedFlushes", "wavePasses", "waveOps", "waveTransposes", "relabels",
                          "globalDiags", "flushes", "marginalPasses", "waveShadowChecks",
-                         "waveShadowMismatches", "permutedOps", "relayouts", "restoreRounds", "swapMicros", "overlappedSwaps", "overlappedPasses")]
+                         "waveShadowMismatches", "permutedOps", "relayouts", "restoreRounds", "swapMicros",
+                         "overlappedSwaps", "overlappedPasses", "layoutAligns")]
 
         self.Complex, self.ComplexMatrix2, self.Vector = Complex, ComplexMatrix2, Vector
         self.ComplexArray, self.QASMLogger, self.Qureg = ComplexArray, QASMLogger, Qureg

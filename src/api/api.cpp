@@ -1200,6 +1200,7 @@ void getQuESTStats(QuESTStats* s) {
     s->swapMicros = be::swapMicros(true);
     s->overlappedSwaps = stats().overlappedSwaps;
     s->overlappedPasses = stats().overlappedPasses;
+    s->layoutAligns = stats().layoutAligns;
 }
 
 void resetQuESTStats(void) {

@@ -257,7 +257,8 @@ void done(const int* peers, int n, hipStream_t producer) {
     // them: a mapping kept until the peer's next token would pin a register
     // the peer may destroy meanwhile, and a destroy-then-create of a register
     // of the same size could then run out of device memory.
-    for (size_t i = 0; i < g_imported.size();) {
+    static const bool keep = getenv("QUEST_IPC_KEEP_STATE") && atoi(getenv("QUEST_IPC_KEEP_STATE"));   // (study)
+    for (size_t i = 0; i < g_imported.size() && !keep;) {
         if (g_imported[i].state) {
             QA_HIP_CHECK(hipIpcCloseMemHandle(g_imported[i].ptr));
             g_imported.erase(g_imported.begin() + (long)i);

@@ -148,9 +148,75 @@ void swapOrder(const QuregImpl& q, const int* gposIn, const int* lposIn, int k, 
     for (int m = 0; m < k; m++) *myG |= chunkBit(q, gpos[m]) << m;
 }
 
-void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn, int k) {
+// Put every rank's local qubits on rank 0's positions.  The ranks' op lists
+// differ -- an op controlled by a rank qubit runs only where that bit is 1, a
+// rank-qubit phase only where it is not 1 -- so their planners may relabel
+// differently, while a swap cuts its parts by position on both sides (the
+// in-place IPC swap even indexes the peer's state with this rank's layout:
+// 8 ranks x 22 qubits, bench seeds 13 / 17 lost norm 1e-5 .. 3e-3 before).
+// One host broadcast per swap; ranks that differ move their qubits with
+// op-free relabelling passes.  Collective.
+void alignLayouts(QuregImpl& q) {
+    static const bool on = !getenv("QUEST_ALIGN_LAYOUTS") || atoi(getenv("QUEST_ALIGN_LAYOUTS")) != 0;   // (0: study)
+    if (!on || !distributed(q)) return;
+    int ref[64];
+    for (int p = 0; p < 64; p++) ref[p] = p < q.nSV ? q.p2l[p] : -1;
+    comm::bcastHost(ref, sizeof ref, 0);
+    bool same = true;
+    for (int p = 0; p < q.L; p++) same = same && ref[p] == q.p2l[p];
+    if (same) return;
+    int want[64];   // rank 0's position of each local logical qubit
+    for (int x = 0; x < 64; x++) want[x] = -1;
+    for (int p = 0; p < q.L; p++) want[ref[p]] = p;
+    int dest[64];
+    for (int p = 0; p < q.L; p++) {
+        dest[p] = want[q.p2l[p]];
+        if (dest[p] < 0) {
+            fprintf(stderr, "QuEST: rank %d holds local qubit %d, rank 0 does not\n", rt().rank, q.p2l[p]);
+            exit(EXIT_FAILURE);
+        }
+    }
+    stats().layoutAligns++;
+    trace::event("align_layout", "\"qubits\": %d", q.nSV);
+    if (be::permuteLocal(q, dest)) {
+        int p2l[64];
+        for (int p = 0; p < q.L; p++) p2l[dest[p]] = q.p2l[p];
+        for (int p = 0; p < q.L; p++) {
+            q.p2l[p] = p2l[p];
+            q.l2p[p2l[p]] = p;
+        }
+        return;
+    }
+    // no relabelling passes on this backend: SWAP ops, position by position
+    static const cplx kSwap[16] = {{1, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 0}, {0, 0},
+                                   {0, 0}, {1, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {1, 0}};
+    for (int i = 0; i < q.L; i++) {
+        if (q.p2l[i] == ref[i]) continue;
+        const int x = q.l2p[ref[i]];   // where rank 0's qubit for position i sits here (local, > i)
+        Op op;
+        op.kind = OpKind::Mat4;
+        op.nt = 2;
+        op.t[0] = i;
+        op.t[1] = x;
+        for (int kk = 0; kk < 16; kk++) op.m[kk] = kSwap[kk];
+        enqueue(q, op);
+        const int li = q.p2l[i];
+        q.l2p[li] = x;
+        q.p2l[x] = li;
+        q.l2p[ref[i]] = i;
+        q.p2l[i] = ref[i];
+    }
+    be::flush(q);
+}
+
+void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn0, int k) {
     if (k <= 0) return;
     be::flush(q);
+    // (the victims are logical qubits: their positions after the alignment)
+    int victims[8], lposIn[8];
+    for (int m = 0; m < k; m++) victims[m] = q.p2l[lposIn0[m]];
+    alignLayouts(q);
+    for (int m = 0; m < k; m++) lposIn[m] = q.l2p[victims[m]];
     trace::Range range("quest.swap");
     be::swapMark(true);
     const double t0 = trace::now();
@@ -405,6 +471,7 @@ void swapWholeChunk(QuregImpl& q, int peer, i64 slice) {
 void restoreChunks(QuregImpl& q) {
     if (chunksIdentity(q)) return;
     be::flush(q);
+    alignLayouts(q);   // whole chunks are exchanged by position
     const int R = q.numChunks, me = rt().rank;
     std::vector<int> f((size_t)R), rounds[2] = {std::vector<int>((size_t)R), std::vector<int>((size_t)R)};
     for (int c = 0; c < R; c++) f[(size_t)q.chunkRank[(size_t)c]] = c;

@@ -100,6 +100,7 @@ struct Stats {
     long long waveShadowChecks = 0, waveShadowMismatches = 0;  // rt().waveShadow
     long long permutedOps = 0;    // inner products / axpby of registers in different layouts, no relayout
     long long relayouts = 0;      // canonicalisations that moved data
+    long long layoutAligns = 0;   // swaps / chunk restores before which this rank moved its local qubits to rank 0's positions
     long long restoreRounds = 0;  // concurrent rounds of whole-chunk exchanges restoring chunk placement
     long long overlappedSwaps = 0;   // swaps issued on their own stream (be::swapOverlapBegin)
     long long overlappedPasses = 0;  // passes started on the part a swap in flight leaves in place

@@ -252,6 +252,43 @@ def layered_wave_relabel(env):
 SCENARIOS["layered_wave_relabel"] = layered_wave_relabel
 
 
+def rank_controlled_relabel(env):
+    """21 qubits (19 local at 4 ranks: wave-sized, front flushes), the bench's
+    layered circuit of seed 13: CNOTs controlled by rank qubits run only on the
+    ranks whose bit is 1, so the ranks' planners see different op lists and
+    relabel differently -- every swap must first bring the ranks' local
+    layouts together (router alignLayouts)."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    import os
+
+    from quest_amd.models.circuits import Circuit
+
+    n = int(os.environ.get("RCR_QUBITS", "21"))
+    r = qa.Register(env, n)
+    r.init_plus()
+    c = random_layered(n, 5, seed=13)
+    per = len(c.gates) // 5 if hasattr(c, "gates") else None
+    ops = list(c.gates) if per else None
+    if ops:   # the bench's windows: one layer, then four (a sync after each)
+        Circuit(n, ops[:per]).apply(r)
+        r.sync()
+        Circuit(n, ops[per:]).apply(r)
+    else:
+        c.apply(r)
+    probs = np.array([r.prob(q, 1) for q in range(n)])
+    amps = np.array([r.amp(i) for i in (0, 1, 777777, (1 << n) - 1)])
+    st = capi.getQuESTStats()
+    out = {"probs": probs, "amps": amps, "norm": r.total_prob(), "_swaps": st["swaps"], "_aligns": st["layoutAligns"]}
+    r.close()
+    return out
+
+
+SCENARIOS["rank_controlled_relabel"] = rank_controlled_relabel
+
+
 def hang_rank1(env):
     """Rank 1 stops responding; rank 0 must give up after QUEST_COMM_TIMEOUT."""
     import time

@@ -357,6 +357,41 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
             assert str(got[k]) == v, k
         else:
             np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+
+
+@pytest.mark.parametrize("transport", ["ipc", "rccl"])
+def test_rank_controlled_relabel_layouts_on_gpu(genv, tmp_path, monkeypatch, transport):
+    """Wave-sized ranks (4 x 22 local qubits on one GPU) whose planners see
+    different op lists -- CNOTs controlled by rank qubits run only where the
+    bit is 1 -- and so relabel differently: every swap first aligns the
+    ranks' local layouts (router alignLayouts).  The in-place IPC swap, which
+    indexes the peer's state with its own layout, lost norm (1e-5 .. 3e-3 on
+    the bench's seeds 13 / 17 at 8 ranks) before; the buffered paths were off
+    by a permutation.  Against the single-rank HIP run."""
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from scenarios import SCENARIOS
+
+    from quest_amd.parallel import spawn_local
+
+    monkeypatch.setenv("RCR_QUBITS", "24")
+    want = SCENARIOS["rank_controlled_relabel"](genv)
+    out = str(tmp_path / "rcr.npz")
+    extra = {"QUEST_BACKEND": "hip", "QUEST_COMM": transport, "PYTHONPATH": os.path.dirname(here),
+             "QUEST_COMM_TIMEOUT": "120", "RCR_QUBITS": "24"}
+    if transport == "rccl":
+        extra["QUEST_RCCL_SHARED_GPU"] = "1"
+    res = spawn_local([os.path.join(here, "dist_worker.py"), "rank_controlled_relabel", out], 4, env_extra=extra,
+                      timeout=200)
+    bad = [(r, p) for r, p in enumerate(res) if p.returncode != 0]
+    assert not bad, "\n".join(f"rank {r} (rc {p.returncode}):\n{p.stdout[-1500:]}\n{p.stderr[-2500:]}" for r, p in bad)
+    with np.load(out, allow_pickle=False) as z:
+        got = {k: z[k] for k in z.files}
+    for k in ("probs", "amps", "norm"):
+        np.testing.assert_allclose(np.asarray(got[k]), np.asarray(want[k]), rtol=0, atol=1e-11, err_msg=k)
+    assert int(got["_swaps"]) > 0
     if name == "restore_chunks":
         # one concurrent round moving one chunk per rank (in place over IPC)
         assert int(got["_xor_rounds"]) == 1
