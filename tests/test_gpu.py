@@ -357,6 +357,10 @@ def test_distributed_equivalence_on_gpu(genv, tmp_path, name, transport, ranks, 
             assert str(got[k]) == v, k
         else:
             np.testing.assert_allclose(np.asarray(got[k]), np.asarray(v), rtol=0, atol=1e-11, err_msg=k)
+    if name == "restore_chunks":
+        # one concurrent round moving one chunk per rank (in place over IPC)
+        assert int(got["_xor_rounds"]) == 1
+        assert int(got["_xor_bytes"]) == 16 * (1 << (9 - {2: 1, 4: 2}[ranks]))
 
 
 @pytest.mark.parametrize("transport", ["ipc", "rccl"])
@@ -392,10 +396,6 @@ def test_rank_controlled_relabel_layouts_on_gpu(genv, tmp_path, monkeypatch, tra
     for k in ("probs", "amps", "norm"):
         np.testing.assert_allclose(np.asarray(got[k]), np.asarray(want[k]), rtol=0, atol=1e-11, err_msg=k)
     assert int(got["_swaps"]) > 0
-    if name == "restore_chunks":
-        # one concurrent round moving one chunk per rank (in place over IPC)
-        assert int(got["_xor_rounds"]) == 1
-        assert int(got["_xor_bytes"]) == 16 * (1 << (9 - {2: 1, 4: 2}[ranks]))
 
 
 IPC_F32 = r'''
