@@ -140,12 +140,16 @@ void phaseOf(const WaveOp& w, double* pr, double* pi) {
     }
 }
 
-// Sign frame (round 5, QUEST_WAVE_ZFRAME=0 to disable): a Z on one register
-// location -- a slot, a real lane bit or a wave bit, the DNEG ops a pass emits
-// for Z / S^2-like gates and for the conditional frame's bookkeeping, 8 % of
-// the bench passes' VALU instructions -- is not executed where it stands but
-// carried along the pass's ops in a set of pending locations and applied once
-// at the end (usually cancelled or absorbed first):
+// Phase frame (round 5, QUEST_WAVE_ZFRAME=0 to disable; QUEST_WAVE_PFRAME=0:
+// signs only): a unit phase on one register location -- a slot, a real lane
+// bit or a wave bit: the DNEG / DMULI / DROT ops a pass emits for Z, S, T, Rz
+// and for the conditional frame's bookkeeping, about a fifth of the bench
+// passes' VALU instructions -- is not executed where it stands but multiplied
+// into the location's pending phase and applied once, where an op needs it or
+// at the end of the pass (phases on one location between two of its gates
+// merge into one op or cancel).  Pending phases commute with diagonal ops and
+// controls and move with transpositions; a 2x2 op on the location applies a
+// general phase first.  A pending sign (Z) goes further:
 //   * diagonal ops and ops controlled by the location commute with it;
 //   * a transposition moves it with the bit (TR swaps two locations);
 //   * a 2x2 op on the location is conjugated instead, U Z = Z (Z U Z): the
@@ -160,30 +164,37 @@ void phaseOf(const WaveOp& w, double* pr, double* pi) {
 // (QUEST_CPU_PLANNER=3) checks it against the oracle like any other plan.
 void zFrame(WaveProgram& out, size_t begin) {
     static const bool on = !getenv("QUEST_WAVE_ZFRAME") || atoi(getenv("QUEST_WAVE_ZFRAME")) != 0;
+    // QUEST_WAVE_PFRAME=0: carry only signs (Z), not general unit phases
+    static const bool phases = !getenv("QUEST_WAVE_PFRAME") || atoi(getenv("QUEST_WAVE_PFRAME")) != 0;
     if (!on || out.ops.size() <= begin) return;
     constexpr int nLoc = kWaveSlots + kWaveLaneBits;   // slots, then lane / wave bits
-    bool z[nLoc] = {false};
-    auto zOp = [](int loc) {
+    double zr[nLoc], zi[nLoc];                         // pending unit phase per location
+    for (int l = 0; l < nLoc; l++) zr[l] = 1, zi[l] = 0;
+    auto pending = [&](int l) { return !(zr[l] == 1 && zi[l] == 0); };
+    auto isZ = [&](int l) { return near(zr[l], -1) && near(zi[l], 0); };
+    std::vector<WaveOp> res(out.ops.begin(), out.ops.begin() + (long)begin);
+    static long long why[4];   // QUEST_ZFRAME_STATS: HADD / 2x2 op, X, channel, end
+    static const bool zst = getenv("QUEST_ZFRAME_STATS") != nullptr;
+    static struct P { ~P() { if (zst) fprintf(stderr, "zframe flushes: op %lld X %lld chan %lld end %lld\n", why[0], why[1], why[2], why[3]); } } printer;
+    int reason = 3;
+    auto flush = [&](int loc) {   // apply the pending phase of loc here
+        if (loc < 0 || loc >= nLoc || !pending(loc)) return;
         WaveOp w;
         memset(&w, 0, sizeof w);
-        w.kind = (int)WKind::DNEG;
-        if (loc < kWaveSlots)
-            w.cReg = 1u << loc;
-        else
-            w.cLane = 1u << (loc - kWaveSlots);
-        return w;
-    };
-    std::vector<WaveOp> res(out.ops.begin(), out.ops.begin() + (long)begin);
-    static long long why[4];   // QUEST_ZFRAME_STATS: HADD, X, channel, end
-    static const bool zst = getenv("QUEST_ZFRAME_STATS") != nullptr;
-    static struct P { ~P() { if (zst) fprintf(stderr, "zframe flushes: H %lld X %lld chan %lld end %lld\n", why[0], why[1], why[2], why[3]); } } printer;
-    int reason = 3;
-    auto flush = [&](int loc) {
-        if (loc >= 0 && loc < nLoc && z[loc]) {
-            res.push_back(zOp(loc));
-            z[loc] = false;
+        int kind;
+        real pm[2] = {0, 0};
+        if (phaseKind(zr[loc], zi[loc], &kind, pm) && kind >= 0) {
+            w.kind = kind;
+            w.m[0] = pm[0];
+            w.m[1] = pm[1];
+            if (loc < kWaveSlots)
+                w.cReg = 1u << loc;
+            else
+                w.cLane = 1u << (loc - kWaveSlots);
+            res.push_back(w);
             if (!t_planQuiet) why[reason]++;
         }
+        zr[loc] = 1, zi[loc] = 0;
     };
     auto single = [](const WaveOp& w, int* loc) {   // one plain control location, nothing else
         if (w.ctrlOut || w.ctrlOutZero || w.cLaneZero || (w.cReg & w.fReg) || (w.cLane & w.fLane)) return false;
@@ -196,12 +207,18 @@ void zFrame(WaveProgram& out, size_t begin) {
         WaveOp w = out.ops[o];
         const WKind k = (WKind)w.kind;
         int loc = -1;
-        if (k == WKind::DNEG && single(w, &loc)) {
-            z[loc] = !z[loc];
+        if ((phases ? isPhaseKind(w.kind) : k == WKind::DNEG) && single(w, &loc)) {
+            double pr, pi;
+            phaseOf(w, &pr, &pi);
+            const double r = zr[loc] * pr - zi[loc] * pi;
+            zi[loc] = zr[loc] * pi + zi[loc] * pr;
+            zr[loc] = r;
+            if (near(zr[loc], 1) && near(zi[loc], 0)) zr[loc] = 1, zi[loc] = 0;   // (cancelled)
             continue;
         }
         if (k == WKind::TR) {
-            std::swap(z[w.a], z[kWaveSlots + w.b]);
+            std::swap(zr[w.a], zr[kWaveSlots + w.b]);
+            std::swap(zi[w.a], zi[kWaveSlots + w.b]);
             res.push_back(w);
             continue;
         }
@@ -221,7 +238,13 @@ void zFrame(WaveProgram& out, size_t begin) {
             continue;
         }
         const int t = slotTarget ? w.a : kWaveSlots + w.a;
-        if (!z[t]) {
+        if (!pending(t)) {
+            res.push_back(w);
+            continue;
+        }
+        if (!isZ(t)) {   // a general phase: applied before the op
+            reason = 0;
+            flush(t);
             res.push_back(w);
             continue;
         }
@@ -244,8 +267,11 @@ void zFrame(WaveProgram& out, size_t begin) {
             case WKind::YSWC: w.kind = (int)WKind::YSW; break;
             case WKind::SWAP: case WKind::LSWAP: {
                 int c = -1;
-                if (single(w, &c)) {
-                    z[c] = !z[c];
+                if (single(w, &c)) {   // CX Z_t = Z_t Z_c CX
+                    const double r = -zr[c];
+                    zi[c] = -zi[c];
+                    zr[c] = r;
+                    if (near(zr[c], 1) && near(zi[c], 0)) zr[c] = 1, zi[c] = 0;
                 } else {
                     reason = 1;
                     flush(t);

@@ -9,7 +9,7 @@ R=$GRAFT_REPO_ROOT
 for v in ${VARIANTS:-full nomem noops}; do
   mkdir -p $R/gpurun_out/po${SEED:-}${TAG:-}/$v
   unset QUEST_LIB QUEST_WAVE_NOOPS
-  [ $v = nomem ] && export QUEST_LIB=$R/quest_amd/lib/var/nomem.so
+  [ $v = nomem ] && export QUEST_LIB=${NOMEM_LIB:-$R/quest_amd/lib/var/nomem.so}
   [ $v = noops ] && export QUEST_WAVE_NOOPS=1
   QUEST_TRACE=$R/gpurun_out/po${SEED:-}${TAG:-}/$v/trace.jsonl timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv \
       -d $R/gpurun_out/po${SEED:-}${TAG:-}/$v -o run -- python3 $R/tools/pass_profile.py run --qubits ${QUBITS:-30} --layers ${LAYERS:-25} --seed ${SEED:-7} \
