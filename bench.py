@@ -194,7 +194,9 @@ def main():
         swap_ms = sum(r["swap_ms"] for r in seed_rows)
         multi = {"swap_ms": swap_ms, "swap_bytes_per_rank": stats["bytesExchanged"],
                  "swap_share": swap_ms / (1e3 * elapsed) if elapsed > 0 else None,
-                 "swap_GBps_per_rank": (stats["bytesExchanged"] / (swap_ms * 1e-3) / 1e9) if swap_ms > 0 else None}
+                 "swap_GBps_per_rank": (stats["bytesExchanged"] / (swap_ms * 1e-3) / 1e9) if swap_ms > 0 else None,
+                 # swaps before which some rank had to bring its local qubits to rank 0's positions
+                 "layout_aligns_max": int(allreduce_max(float(stats["layoutAligns"])))}
     result = {
         "metric": "single-qubit-gate time (s) vs #qubits, fp64 state-vector; 1/2/4/8-GPU scaling",
         "value": s_per_gate,
