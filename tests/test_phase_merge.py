@@ -61,8 +61,8 @@ assert st["wavePasses"] >= 1, st
 '''
 
 
-def _run(backend, merge, tol, n):
-    env = dict(os.environ, QUEST_BACKEND=backend, QUEST_WAVE_MERGE_PHASES=merge)
+def _run(backend, merge, tol, n, **knobs):
+    env = dict(os.environ, QUEST_BACKEND=backend, QUEST_WAVE_MERGE_PHASES=merge, **knobs)
     if backend == "cpu":
         env["QUEST_CPU_PLANNER"] = "3"
     out = subprocess.run([sys.executable, "-c", SCRIPT.replace("TOL", repr(tol)), str(n)], cwd=ROOT, env=env,
@@ -87,3 +87,23 @@ def test_phase_merge_on_the_wave_emulation():
 @pytest.mark.gpu
 def test_phase_merge_gpu():
     _check("hip", 1e-12, 20)   # the GPU takes the wave engine from 19 local qubits
+
+
+def _check_frame(backend, tol, n):
+    """The phase frame (zFrame in src/core/wave.cpp): single-location phases
+    carried along the pass and merged per location, signs absorbed by the 2x2
+    ops and CNOTs after them.  Same plans, fewer wave ops, the oracle's state."""
+    ops_p, passes_p = _run(backend, "1", tol, n)
+    ops_z, passes_z = _run(backend, "1", tol, n, QUEST_WAVE_PFRAME="0")
+    ops_0, passes_0 = _run(backend, "1", tol, n, QUEST_WAVE_ZFRAME="0")
+    assert passes_p == passes_z == passes_0
+    assert ops_p < ops_z <= ops_0, (ops_p, ops_z, ops_0)
+
+
+def test_phase_frame_on_the_wave_emulation():
+    _check_frame("cpu", 1e-12, 16)
+
+
+@pytest.mark.gpu
+def test_phase_frame_gpu():
+    _check_frame("hip", 1e-12, 20)
