@@ -752,10 +752,15 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
             std::vector<Op> mine = ops;
             TileProgram prog;
             planTiles(mine, L, kWaveBits, c, true, prog, kWaveVecBits, &h);
+            // score: sum over passes of max(C, M) + alpha min(C, M) -- a one-tile
+            // workgroup overlaps compute and memory worst when they are close
+            // (round 5: T = 1.2 sum max with C near M); QUEST_PLAN_SCORE_OVERLAP = alpha
+            static const double alpha = getenv("QUEST_PLAN_SCORE_OVERLAP") ? atof(getenv("QUEST_PLAN_SCORE_OVERLAP")) : 0.0;
             double t = 0;
             for (const TilePass& ps : prog.passes) {
                 const double cyc = wavePassCycles(ps, prog.ops.data() + ps.opBegin);
-                t += std::max(cyc < 0 ? M : cyc, M);
+                const double c = cyc < 0 ? M : cyc;
+                t += std::max(c, M) + alpha * std::min(c, M);
             }
             score[i] = t;
         }
