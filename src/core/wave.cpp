@@ -539,6 +539,30 @@ struct CnotStatsPrinter {
                                 g_cnotStats[r][c][t], 100.0 * g_cnotStats[r][c][t] / tot);
     }
 } g_cnotStatsPrinter;
+// QUEST_CTRL_STATS=1 (kernel study): ops of the executed wave passes by kind
+// and slot-control count (0, 1, 2+) / lane controls, with modeled cycles
+long long g_ctrlOps[32][3][2];
+double g_ctrlCyc[32][3][2];
+bool ctrlStatsOn() {
+    static const bool on = getenv("QUEST_CTRL_STATS") != nullptr;
+    return on;
+}
+struct CtrlStatsPrinter {
+    ~CtrlStatsPrinter() {
+        if (!ctrlStatsOn()) return;
+        double tot = 0;
+        for (auto& a : g_ctrlCyc)
+            for (auto& b : a)
+                for (double v : b) tot += v;
+        fprintf(stderr, "wave ops by kind / slot controls / lane controls (modeled cycles %.3g):\n", tot);
+        for (int k = 0; k < 32; k++)
+            for (int c = 0; c < 3; c++)
+                for (int l = 0; l < 2; l++)
+                    if (g_ctrlOps[k][c][l])
+                        fprintf(stderr, "  kind %2d cReg %d%s lanes %d %8lld ops %5.1f %% cycles\n", k, c, c == 2 ? "+" : " ", l,
+                                g_ctrlOps[k][c][l], 100.0 * g_ctrlCyc[k][c][l] / tot);
+    }
+} g_ctrlStatsPrinter;
 }  // namespace
 thread_local int t_planQuiet = 0;
 thread_local int t_waveCframe = -1;
@@ -1859,6 +1883,13 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     for (int s = 0; s < kWaveSlots; s++) wp.stSlot[s] = lay.slotBit[s];
     for (int l = 0; l < kWaveLaneBits; l++) wp.stLane[l] = lay.laneBit[l];
     zFrame(out, (size_t)wp.opBegin);
+    if (ctrlStatsOn() && !t_planQuiet)
+        for (size_t o = (size_t)wp.opBegin; o < out.ops.size(); o++) {
+            const WaveOp& w = out.ops[o];
+            const int pc = __builtin_popcount(w.cReg), c = pc > 2 ? 2 : pc, l = (w.cLane & 63u) ? 1 : 0;
+            g_ctrlOps[w.kind & 31][c][l]++;
+            g_ctrlCyc[w.kind & 31][c][l] += waveOpCycles(w);
+        }
     wp.opEnd = (int)out.ops.size();
     for (int o = wp.opBegin; o < wp.opEnd; o++)
         wp.waveExchange = wp.waveExchange || (out.ops[(size_t)o].kind == (int)WKind::TR && out.ops[(size_t)o].b >= kWaveLanes);

@@ -144,7 +144,10 @@ def set_layout(R):
              ("trw", 4 * R), ("lane", 8 * len(LANE_KINDS)), ("slot2", len(KINDS2) * 2 * R),
              ("ph", len(PH_KINDS) * 2 * NS), ("ch", len(CH_KINDS) * R * R),
              # controls on lane bits only (cReg 0): exec set once, no per-register tests
-             ("slotL", len(KINDS) * R), ("slot2L", len(KINDS2) * R), ("d2sL", R)]
+             ("slotL", len(KINDS) * R), ("slot2L", len(KINDS2) * R), ("d2sL", R),
+             # X on slot s / lane bit l with ONE slot control c of polarity v
+             # (CNOTs): the registers fixed at generation time, no per-register tests
+             ("swk", R * R * 2 + LANE_BITS * R * 2)]
     LAYOUT.clear()
     LAYOUT["R"] = R
     i = 0
@@ -158,6 +161,13 @@ def idx_slot(kind, s, ctrl):
     if ctrl == 2:
         return LAYOUT["slotL"] + KINDS.index(kind) * LAYOUT["R"] + s
     return LAYOUT["slot"] + KINDS.index(kind) * 2 * LAYOUT["R"] + s * 2 + ctrl
+
+
+def idx_swk(lane, t, c, v):
+    """X on slot t (lane = 0) or lane bit t (lane = 1) controlled by slot c
+    being v."""
+    R = LAYOUT["R"]
+    return LAYOUT["swk"] + (R * R * 2 if lane else 0) + (t * R + c) * 2 + v
 
 
 def idx_d2s(s, ctrl):
@@ -720,6 +730,33 @@ class Gen:
         else:
             self.end_region()
         self.lane_ctrl_end()
+        self.back()
+
+    def gen_swk(self, lane, t, c, v):
+        """X on slot t (lane = 0) or on lane bit t (lane = 1) of the registers
+        j whose slot-c bit is v: a CNOT whose control sits in a slot.  The
+        generic controlled handler tests every register's bit of the record's
+        mask (32 scalar tests, up to 16 taken branches, its moves unscheduled);
+        here the registers are fixed, the moves list-scheduled.  Lane controls
+        still set exec (ctrl_begin)."""
+        self.handler(idx_swk(lane, t, c, v), f"SWK_{'l' if lane else 's'}{t}_c{c}_v{v}")
+        e = self.e
+        if lane:
+            e("s_nop 1")
+        self.ctrl_begin()
+        if lane:
+            for j in range(self.NS):
+                if ((j >> c) & 1) != v:
+                    continue
+                for r in [self.re(j) + d for d in range(self.P)] + [self.im(j) + d for d in range(self.P)]:
+                    e(f"ds_swizzle_b32 v{r}, v{r} offset:{0x1f | ((1 << t) << 10):#x}")
+        else:
+            self.region()
+            for j in range(self.NS):
+                if not (j >> t) & 1 and ((j >> c) & 1) == v:
+                    self.pair("SWAP", j, j | (1 << t))
+            self.end_region()
+        self.ctrl_end()
         self.back()
 
     def swap_pairs32(self, s):
@@ -1482,6 +1519,12 @@ class Gen:
             for creg in range(NS):
                 for lane in (0, 1):
                     self.gen_ph(kind, creg, lane)
+        for lane, nt in ((0, R), (1, LANE_BITS if SWZ >= 2 else 0)):   # (lane variants: swizzle exchange only)
+            for t in range(nt):
+                for c in range(R):
+                    if lane or c != t:
+                        for v in (0, 1):
+                            self.gen_swk(lane, t, c, v)
         self.finish_handler()
         L.append(".Lfunc_end0:")
         L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
@@ -1767,7 +1810,7 @@ def main():
         f.write(f"static const int kWaveImageVgprs = {vg.group(1)};\n")
         set_layout(args.slots)
         f.write(f"static const int kWaveImagePrec = {args.prec};\n")
-        for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch", "slotL", "slot2L", "d2sL"):
+        for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch", "slotL", "slot2L", "d2sL", "swk"):
             f.write(f"static const int kWaveIdx_{k} = {LAYOUT[k]};\n")
         f.write(f"static const int kWaveSentinelIndex = {LAYOUT['done']};\n")
         f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
