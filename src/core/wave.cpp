@@ -543,6 +543,7 @@ struct CnotStatsPrinter {
 // and slot-control count (0, 1, 2+) / lane controls, with modeled cycles
 long long g_ctrlOps[32][3][2];
 double g_ctrlCyc[32][3][2];
+double g_trByBit[16][2];   // TR ops by lane / wave bit: count, modeled cycles
 bool ctrlStatsOn() {
     static const bool on = getenv("QUEST_CTRL_STATS") != nullptr;
     return on;
@@ -561,6 +562,9 @@ struct CtrlStatsPrinter {
                     if (g_ctrlOps[k][c][l])
                         fprintf(stderr, "  kind %2d cReg %d%s lanes %d %8lld ops %5.1f %% cycles\n", k, c, c == 2 ? "+" : " ", l,
                                 g_ctrlOps[k][c][l], 100.0 * g_ctrlCyc[k][c][l] / tot);
+        for (int b = 0; b < 16; b++)
+            if (g_trByBit[b][0] > 0)
+                fprintf(stderr, "  TR with bit %2d: %6.0f ops %5.1f %% cycles\n", b, g_trByBit[b][0], 100.0 * g_trByBit[b][1] / tot);
     }
 } g_ctrlStatsPrinter;
 }  // namespace
@@ -1888,6 +1892,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
             const WaveOp& w = out.ops[o];
             const int pc = __builtin_popcount(w.cReg), c = pc > 2 ? 2 : pc, l = (w.cLane & 63u) ? 1 : 0;
             g_ctrlOps[w.kind & 31][c][l]++;
+            if (w.kind == (int)WKind::TR) g_trByBit[w.b & 15][0]++, g_trByBit[w.b & 15][1] += waveOpCycles(w);
             g_ctrlCyc[w.kind & 31][c][l] += waveOpCycles(w);
         }
     wp.opEnd = (int)out.ops.size();

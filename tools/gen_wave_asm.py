@@ -147,7 +147,9 @@ def set_layout(R):
              ("slotL", len(KINDS) * R), ("slot2L", len(KINDS2) * R), ("d2sL", R),
              # X on slot s / lane bit l with ONE slot control c of polarity v
              # (CNOTs): the registers fixed at generation time, no per-register tests
-             ("swk", R * R * 2 + LANE_BITS * R * 2)]
+             ("swk", R * R * 2 + LANE_BITS * R * 2),
+             # the shared check path of ops with tile / wave predicates
+             ("check", 1)]
     LAYOUT.clear()
     LAYOUT["R"] = R
     i = 0
@@ -475,8 +477,9 @@ class Gen:
             else:
                 pro.append(f"\ts_mov_b32 s{d}, s{d - 32}")
                 k += 1
+        # (the host keeps the op records inside one 4 GiB-aligned window: no
+        # carry into s95)
         pro += ["\ts_add_u32 s94, s94, 96",
-                "\ts_addc_u32 s95, s95, 0",
                 "\ts_load_dwordx8 s[36:43], s[94:95], 0x0",
                 "\ts_load_dwordx16 s[44:59], s[94:95], 0x20"]
         self.lines[self.hstart:self.hstart] = pro
@@ -495,47 +498,47 @@ class Gen:
         the shared check path (rare)."""
         e = self.e
         e("s_waitcnt lgkmcnt(0)")
-        # flagged ops (bit 31) go to the shared check path: selected as the
-        # jump target rather than branched to (handlers lie > 128 KiB away)
-        e("s_bitcmp1_b32 s36, 31")
-        e("s_cselect_b32 s98, .Lcheck-qa_wave_tile, s36")
-        e("s_add_u32 s98, s92, s98")                   # kernel base + handler offset
+        # (ops with tile / wave predicates name the shared check path as their
+        # handler; their own handler rides in the record's cWave word)
+        e("s_add_u32 s98, s92, s36")                   # kernel base + handler offset
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
 
     def check_path(self):
-        """Shared slow path of next_op: skip the op (prefetch the one after
-        it and start that) unless the tile satisfies its out-of-tile controls
-        and this wave its wave-bit controls, else dispatch it.  The record is
-        still in the prefetch buffer s[36:59]."""
+        """Shared slow path (handler table entry "check"): an op with tile or
+        wave predicates names it as its handler.  Skip the op (prefetch the one
+        after it and start that) unless the tile satisfies its out-of-tile
+        controls and this wave its wave-bit controls, else jump to the op's own
+        handler, bits 8.. of the cWave word (s42; bits 0-7 the wave bits).
+        The record is still in the prefetch buffer s[36:59]."""
         e = self.e
-        self.label(".Lcheck")
+        self.label("wh_CHECK")
+        self.handlers[LAYOUT["check"]] = "wh_CHECK"
         e("s_and_b64 s[96:97], s[32:33], s[40:41]")    # ctrlOut of the op
         e("s_cmp_eq_u64 s[96:97], s[40:41]")
         e("s_cbranch_scc0 .Lskip_op")
-        # handler bit 30: out-of-tile bits that must be 0 in record bytes
+        # cWaveZero bit 31: out-of-tile bits that must be 0 in record bytes
         # 48-55 (a DIAG's spare m[2]; folded diagonal runs)
-        e("s_bitcmp1_b32 s36, 30")
+        e("s_bitcmp1_b32 s43, 31")
         e("s_cbranch_scc0 .Lcheck_zero_done")
         e("s_and_b64 s[96:97], s[32:33], s[48:49]")
         e("s_cmp_eq_u64 s[96:97], 0")
         e("s_cbranch_scc0 .Lskip_op")
         self.label(".Lcheck_zero_done")
         if self.W:
-            e("s_and_b32 s96, s3, s42")                 # wave bits that must be 1
-            e("s_cmp_eq_u32 s96, s42")
+            e("s_and_b32 s97, s42, 0xff")
+            e("s_and_b32 s96, s3, s97")                 # wave bits that must be 1
+            e("s_cmp_eq_u32 s96, s97")
             e("s_cbranch_scc0 .Lskip_op")
             e("s_and_b32 s96, s3, s43")                 # wave bits that must be 0
             e("s_cmp_eq_u32 s96, 0")
             e("s_cbranch_scc0 .Lskip_op")
-        e("s_bitset0_b32 s36, 31")
-        e("s_bitset0_b32 s36, 30")
-        e("s_add_u32 s98, s92, s36")
+        e("s_lshr_b32 s98, s42, 8")
+        e("s_add_u32 s98, s92, s98")
         e("s_addc_u32 s99, s93, 0")
         e("s_setpc_b64 s[98:99]")
         self.label(".Lskip_op")
         e("s_add_u32 s94, s94, 96")
-        e("s_addc_u32 s95, s95, 0")
         e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
         e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
         e("s_branch .Lnext")
@@ -1810,7 +1813,7 @@ def main():
         f.write(f"static const int kWaveImageVgprs = {vg.group(1)};\n")
         set_layout(args.slots)
         f.write(f"static const int kWaveImagePrec = {args.prec};\n")
-        for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch", "slotL", "slot2L", "d2sL", "swk"):
+        for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch", "slotL", "slot2L", "d2sL", "swk", "check"):
             f.write(f"static const int kWaveIdx_{k} = {LAYOUT[k]};\n")
         f.write(f"static const int kWaveSentinelIndex = {LAYOUT['done']};\n")
         f.write(f"static const int kWaveHandlerOffset[{len(table)}] = {{{', '.join(map(str, table))}}};\n")
