@@ -128,6 +128,10 @@ SEL = "s[98:99]"
 # DPP / v_permlane*_swap for all; through LDS measured slower, 0.139 ->
 # 0.146-0.163 ms / gate for lane bits 0 / 0-1 / 0-3, profiles/r3/tr_lds_ab.txt)
 TR_LDS = int(_os.environ.get("WAVE_TR_LDS", "0"))
+# lane-control exec masks: s_mov_b64 exec straight after the v_cmp that writes
+# its SGPR pair (no s_nop: SALU reads of VALU-written SGPRs are interlocked;
+# WAVE_EXEC_NOP=1 restores the pad)
+NOP_FREE_EXEC = _os.environ.get("WAVE_EXEC_NOP", "0") != "1"
 
 
 # op record fields live in s[36:59] (prefetch buffer) and s[68:91] (the
@@ -551,8 +555,9 @@ class Gen:
         self.e(f"v_xor_b32_e32 v{self.vTmp}, s71, v{self.vLane}")   # aux: lane bits the planner flipped
         self.e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vTmp}")
         self.e(f"v_cmp_eq_u32_e64 s[96:97], s70, v{self.vTmp}")
-        self.e("s_nop 4")
-        self.e("s_mov_b64 exec, s[96:97]")
+        if not NOP_FREE_EXEC:
+            self.e("s_nop 4")
+        self.e("s_mov_b64 exec, s[96:97]")   # (an SALU read of a VALU-written SGPR is interlocked)
 
     def ctrl_j(self, j, skip):
         self.e(f"s_bitcmp1_b32 s69, {j}")
@@ -832,7 +837,8 @@ class Gen:
             e(f"v_xor_b32_e32 v{self.vTmp}, s71, v{self.vLane}")
             e(f"v_and_b32_e32 v{self.vTmp}, s70, v{self.vTmp}")
             e(f"v_cmp_eq_u32_e64 s[96:97], s70, v{self.vTmp}")
-            e("s_nop 4")
+            if not NOP_FREE_EXEC:
+                e("s_nop 4")
             e("s_mov_b64 exec, s[96:97]")
         self.region()
         js = [j for j in range(self.NS) if (j & creg) == creg]
