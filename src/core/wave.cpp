@@ -672,6 +672,7 @@ struct WaveStrategy {
     double look;   // one-pass lookahead weight (< 0: default)
     int cframe;    // conditional exchange frame: 1 as configured, 0 off
     int commute;   // class-aware commutation in the scheduler (t_planCommute): -1 as configured, 0 off, 1 on
+    double mem = 0;  // trimming bound in modeled cycles (0: waveCostHooks')
 };
 // 0 is the configured default (cost = -1, cframe = -1: waveCostHooks and the
 // environment as they are); the 8th is the round-3 planner (no compute-aware
@@ -680,13 +681,17 @@ const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1, -1}, {1, 1, 0, -1, 1, -1}
                                     {1, 0, 0, -1, 1, -1},   {0, 2, 0, -1, 1, -1},  {0, 1, 48, -1, 1, -1},
                                     {0, 1, 0, 0.5, 1, -1},  {0, 0, 0, -1, 0, -1},  {0, -1, 0, -1, -1, 1},
                                     {1, 1, 0, -1, 1, 1},    {0, 0, 0, -1, 1, 1},   {1, 0, 0, -1, 1, 1},
-                                    {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1}};
+                                    {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1},  {0, 1, 0, -1, 1, -1, 15000},
+                                    {0, 1, 0, -1, 1, -1, 17500}};
 constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
-// strategies the search tries (QUEST_PLAN_STRATEGIES, default all 14: with
+// strategies the search tries (QUEST_PLAN_STRATEGIES, default all 16: with
 // the commutation and one-fewer-resident-position variants the five bench
 // seeds plan 80 passes instead of 82, 0.1306 vs 0.1317 ms / gate over three
 // interleaved rounds on one box, profiles/r5/search_strategies_ab.txt; 11
-// circuit seeds 177 instead of 183 passes in the host model)
+// circuit seeds 177 instead of 183 passes in the host model; the last two,
+// trimming against a larger memory budget, leave the bench seeds' plans as
+// they are and take fresh seeds 14-20 from 96 to 94 passes, 0.1247 -> 0.1233
+// ms / gate, profiles/r5/trim_budget_strategies_ab.txt)
 int searchStrategies() {
     static const int n = [] {
         const char* e = getenv("QUEST_PLAN_STRATEGIES");
@@ -712,7 +717,7 @@ void strategyHooks(const WaveStrategy& st, PlanHooks& h) {
     h.memCost = 0;
     if (st.cost) {
         h.passCost = [](const TilePass& ps, const TileOp* o) { return wavePassCycles(ps, o); };
-        h.memCost = M;
+        h.memCost = st.mem > 0 ? st.mem : M;
         h.costMargin = st.cost == 2 ? 0.0 : costed.costMargin;
     }
     h.seeds = st.seeds;

@@ -16,6 +16,28 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, HERE)
 
 
+def _free_port_pair():
+    """A port P with P + 1 free as well: torchrun's store listens on P, the
+    QuEST bootstrap on MASTER_PORT + 1 (src/comm/bootstrap.cpp) -- under
+    parallel test workers another test's listener on P + 1 made the ranks
+    greet the wrong process."""
+    import socket
+
+    for _ in range(64):
+        a, b = socket.socket(), socket.socket()
+        try:
+            a.bind(("127.0.0.1", 0))
+            port = a.getsockname()[1]
+            b.bind(("127.0.0.1", port + 1))
+            return port
+        except OSError:
+            continue
+        finally:
+            a.close()
+            b.close()
+    raise RuntimeError("no free port pair")
+
+
 def _single(name, env):
     from scenarios import SCENARIOS
 
@@ -143,15 +165,11 @@ def test_bench_under_torchrun_host_build():
     127.0.0.1 rendezvous) on the host build: one JSON line from rank 0 with
     n_gpus 4, the state sharded over 4 ranks and qubit swaps performed."""
     import json
-    import socket
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = _free_port_pair()
     env = dict(os.environ, QUEST_BACKEND="cpu", OMP_NUM_THREADS="1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "QUEST_BOOTSTRAP_PORT"):
         env.pop(k, None)
@@ -176,15 +194,11 @@ def test_swap_victims_survive_relabelling():
     and a second full swap followed (2 instead of 1 per window at 2 ranks, 3
     instead of 1 at 8 ranks on the GPU)."""
     import json
-    import socket
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = _free_port_pair()
     env = dict(os.environ, QUEST_BACKEND="cpu", QUEST_CPU_PLANNER="3", QUEST_PLAN_ONLY="1", OMP_NUM_THREADS="2")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "QUEST_BOOTSTRAP_PORT"):
         env.pop(k, None)

@@ -130,6 +130,30 @@ def test_fp32_wave_matches_fp64_layered_24q_gpu():
 
 
 @pytest.mark.gpu
+def test_static_ctrl_cnot_handlers_match_generic_gpu():
+    """CNOTs with one slot control (both polarities: X gates before them put
+    their control bits in the exchange frame) through the fixed-register swk
+    handlers give bit-for-bit the state of the generic mask-tested handler
+    (QUEST_WAVE_STATIC_CTRL=0): the two only move data."""
+    code = ("import numpy as np, quest_amd as qa\n"
+            "from quest_amd.models import random_layered\n"
+            "e = qa.Env(); r = qa.Register(e, 22); r.init_plus(); qa.capi.resetQuESTStats()\n"
+            "random_layered(22, 12, seed=11).apply(r); r.sync()\n"
+            "st = qa.capi.getQuESTStats(); assert st['wavePasses'] > 0, st\n"
+            "np.save('{out}', r.to_numpy())\n")
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        res = {}
+        for v in ("0", "1"):
+            f = os.path.join(d, f"s{v}.npy")
+            out = _run(["-c", code.format(out=f)], {"QUEST_WAVE_STATIC_CTRL": v, "QUEST_BACKEND": "hip"}, timeout=300)
+            assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+            res[v] = np.load(f)
+        assert np.array_equal(res["0"], res["1"])
+        assert abs(np.vdot(res["1"], res["1"]).real - 1) < 1e-12
+
+
+@pytest.mark.gpu
 def test_wave_kernel_matches_lds_kernel_gpu(env):
     import quest_amd as qa
     from quest_amd.models import random_layered
