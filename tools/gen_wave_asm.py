@@ -134,8 +134,9 @@ TR_LDS = int(_os.environ.get("WAVE_TR_LDS", "0"))
 NOP_FREE_EXEC = _os.environ.get("WAVE_EXEC_NOP", "0") != "1"
 
 
-# op record fields live in s[36:59] (prefetch buffer) and s[68:91] (the
-# running handler's copy): handler, cReg, cLane, aux, ctrlOut (2), cWave,
+# op record fields live in s[36:51] (prefetch buffer: record bytes 0-63) and
+# s[68:91] (the running handler's copy; bytes 64-95 loaded by the handlers
+# that read them): handler, cReg, cLane, aux, ctrlOut (2), cWave,
 # cWaveZero, m[8] (fp64) / m[16] (fp32)
 REC_LO, REC_HI = 68, 91
 
@@ -471,7 +472,12 @@ class Gen:
             for a in re.findall(r"\bs(\d+)\b", ln):
                 used.add(int(a))
         used = sorted(d for d in used if REC_LO <= d <= REC_HI)
-        pro = []
+        # record bytes 64-95 (s84..s91: fp64 m[4..7], read by general 2x2s and
+        # channels) are not prefetched: a handler that reads them loads them
+        # from its own record here, beside the next record's prefetch
+        hi = [d for d in used if d >= REC_HI - 7]
+        used = [d for d in used if d < REC_HI - 7]
+        pro = [f"\ts_load_dwordx8 s[{REC_HI - 7}:{REC_HI}], s[94:95], 0x40"] if hi else []
         k = 0
         while k < len(used):
             d = used[k]
@@ -484,8 +490,9 @@ class Gen:
         # (the host keeps the op records inside one 4 GiB-aligned window: no
         # carry into s95)
         pro += ["\ts_add_u32 s94, s94, 96",
-                "\ts_load_dwordx8 s[36:43], s[94:95], 0x0",
-                "\ts_load_dwordx16 s[44:59], s[94:95], 0x20"]
+                "\ts_load_dwordx16 s[36:51], s[94:95], 0x0"]
+        if hi:
+            pro.append("\ts_waitcnt lgkmcnt(0)")
         self.lines[self.hstart:self.hstart] = pro
         self.hstart = None
 
@@ -543,8 +550,7 @@ class Gen:
         e("s_setpc_b64 s[98:99]")
         self.label(".Lskip_op")
         e("s_add_u32 s94, s94, 96")
-        e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
-        e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
+        e("s_load_dwordx16 s[36:51], s[94:95], 0x0")   # (record bytes 0-63; see finish_handler)
         e("s_branch .Lnext")
 
     # ---- predication: exec = lanes whose controls hold; registers j whose
@@ -1461,8 +1467,7 @@ class Gen:
             e("s_waitcnt vmcnt(0)")
         # ---- op loop: prefetch op 0, then every op starts through next_op()
         e("s_mov_b64 s[94:95], s[10:11]")
-        e("s_load_dwordx8 s[36:43], s[94:95], 0x0")
-        e("s_load_dwordx16 s[44:59], s[94:95], 0x20")
+        e("s_load_dwordx16 s[36:51], s[94:95], 0x0")
         self.label(".Lnext")
         self.next_op()
         self.check_path()
