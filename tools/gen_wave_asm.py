@@ -511,9 +511,8 @@ class Gen:
         e("s_waitcnt lgkmcnt(0)")
         # (ops with tile / wave predicates name the shared check path as their
         # handler; their own handler rides in the record's cWave word)
-        e("s_add_u32 s98, s92, s36")                   # kernel base + handler offset
-        e("s_addc_u32 s99, s93, 0")
-        e("s_setpc_b64 s[98:99]")
+        e("s_add_u32 s18, s92, s36")                   # kernel base + handler offset (no carry: host-checked)
+        e("s_setpc_b64 s[18:19]")
 
     def check_path(self):
         """Shared slow path (handler table entry "check"): an op with tile or
@@ -544,10 +543,9 @@ class Gen:
             e("s_and_b32 s96, s3, s43")                 # wave bits that must be 0
             e("s_cmp_eq_u32 s96, 0")
             e("s_cbranch_scc0 .Lskip_op")
-        e("s_lshr_b32 s98, s42, 8")
-        e("s_add_u32 s98, s92, s98")
-        e("s_addc_u32 s99, s93, 0")
-        e("s_setpc_b64 s[98:99]")
+        e("s_lshr_b32 s18, s42, 8")
+        e("s_add_u32 s18, s92, s18")
+        e("s_setpc_b64 s[18:19]")
         self.label(".Lskip_op")
         e("s_add_u32 s94, s94, 96")
         e("s_load_dwordx16 s[36:51], s[94:95], 0x0")   # (record bytes 0-63; see finish_handler)
@@ -1373,6 +1371,23 @@ class Gen:
         e("s_sub_u32 s92, s92, .Lentry_pc-qa_wave_tile")   # kernel base: handlers jump from here
         e("s_subb_u32 s93, s93, 0")
         e("s_waitcnt lgkmcnt(0)")
+        # launch word bit 29: report the kernel base (vector stores of every
+        # lane to debugBuf) and stop -- the host checks once that no handler
+        # address carries into the high word, which next_op then never adds
+        e("s_load_dword s52, s[8:9], 0x14")
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_bitcmp1_b32 s52, 29")
+        e("s_cbranch_scc0 .Lno_base_probe")
+        e(f"s_load_dwordx2 s[52:53], s[8:9], {DEBUG_BUF}")
+        e("s_waitcnt lgkmcnt(0)")
+        e("v_mov_b32_e32 v128, s92")
+        e("v_mov_b32_e32 v129, s93")
+        e("v_mov_b32_e32 v130, 0")
+        e("global_store_dwordx2 v130, v[128:129], s[52:53]")
+        e("s_waitcnt vmcnt(0)")
+        e("s_endpgm")
+        self.label(".Lno_base_probe")
+        e("s_mov_b32 s19, s93")                       # handler addresses: s[18:19] = {s92 + offset, s93}
         e("s_load_dwordx4 s[12:15], s[8:9], 0x0")     # numTiles, waveStride
         e("s_load_dwordx8 s[20:27], s[8:9], 0x18")    # pos[0..7]
         e("s_load_dwordx4 s[28:31], s[8:9], 0x38")    # pos[8..11]
