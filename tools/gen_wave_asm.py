@@ -128,6 +128,11 @@ SEL = "s[98:99]"
 # DPP / v_permlane*_swap for all; through LDS measured slower, 0.139 ->
 # 0.146-0.163 ms / gate for lane bits 0 / 0-1 / 0-3, profiles/r3/tr_lds_ab.txt)
 TR_LDS = int(_os.environ.get("WAVE_TR_LDS", "0"))
+# s_nop 3 pads after every tile load: the loads' issue paced (bench -0.4 %
+# with one, neutral with three, profiles/r5/load_pacing_ab.txt; issuing them
+# back to back -- the re / im bases hoisted out of the per-group address adds
+# -- was 1.3 % slower, group_base_hoist_ab.txt)
+LD_PACE = int(_os.environ.get("WAVE_LD_PACE", "1"))
 # lane-control exec masks: s_mov_b64 exec straight after the v_cmp that writes
 # its SGPR pair (no s_nop: SALU reads of VALU-written SGPRs are interlocked;
 # WAVE_EXEC_NOP=1 restores the pad)
@@ -1692,6 +1697,8 @@ class Gen:
                     continue
                 if what == "ld":
                     e(f"buffer_load_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen{LD_POLICY}")
+                    for _ in range(LD_PACE):
+                        e("s_nop 3")
                 else:
                     e(f"buffer_store_dwordx4 v[{base}:{base + 3}], v{vb}, s[{Q}:{Q + 3}], 0 offen{ST_POLICY}")
         if prio:
