@@ -537,8 +537,10 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
     // put at the victim's old position, a needless later swap).
     static const bool early = !getenv("QUEST_SWAP_EARLY") || atoi(getenv("QUEST_SWAP_EARLY")) != 0;
     int gp[8], lp[8], k = 0;
+    int vlog[8];   // early victims as logical qubits: the flush below may still relabel them
     if (early) {
         k = chooseVictims(q, lq, be::queuedTargets(q), gp, lp);
+        for (int m = 0; m < k; m++) vlog[m] = q.p2l[lp[m]];
         static const bool dbg = getenv("QUEST_SWAP_DEBUG") != nullptr;
         if (dbg)
             fprintf(stderr, "rank %d swap: victims chosen %s the flush (%zu ops queued)\n", rt().rank,
@@ -565,6 +567,12 @@ void planSwap(QuregImpl& q, const std::vector<Op>& lq) {
     }
     be::flush(q);
     q.nSwapVictims = 0;
+    // (queuedTargets keeps the victims off the positions every tile holds for
+    // the default planner only -- cmin <= 8; a larger QUEST_WAVE_CMIN or a
+    // search strategy with one more resident position can relabel them: the
+    // swap takes the logical victims wherever the flush left them, the same
+    // qubits on every rank)
+    for (int m = 0; m < k; m++) lp[m] = q.l2p[vlog[m]];
     if (k == 0) k = chooseVictims(q, lq, 0, gp, lp);
     if (k == 0) {
         fprintf(stderr, "QuEST: no local qubit available for a distributed swap\n");

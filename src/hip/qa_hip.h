@@ -47,6 +47,7 @@ struct Tuning {
     int directLowToTile = 0;  // 1: ops on bits inside a 128-byte line go to the tile pass (0: in-vector / lane-shuffle kernels)
     int tileQubits = 0;     // tile bits of fused passes (0: kTileQubits; kTileQubits + 1 = 64 KiB tiles)
     int waveTileMap = 0;    // wave kernel: XCD / CU-aware tile order (QUEST_WAVE_TILE_MAP)
+    int waveDynamic = 1;    // looping wave grids claim tiles through an atomic counter (QUEST_WAVE_DYNAMIC)
 };
 Tuning& tuning();
 

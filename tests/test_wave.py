@@ -176,6 +176,36 @@ def test_wave_kernel_matches_lds_kernel_gpu(env):
     assert np.max(np.abs(outs[0] - outs[3])) < 1e-12
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [24, 25])
+def test_looping_grids_match_one_tile_grid_gpu(env, n):
+    """Looping wave grids (workgroups that claim tiles from a counter, and
+    with a --pfa / --pfl image the next-tile prefetch: tools/gen_wave_asm.py
+    dyn_claim / pf_paths) give bit for bit the state of one workgroup per
+    tile and of the static stride (QUEST_WAVE_DYNAMIC=0).  24 and 25 qubits:
+    2048 / 4096 tiles over 768 resident workgroups (uneven claims)."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.ops import capi
+
+    outs = {}
+    for name, per, dyn in (("one", 0, 1), ("static", 3, 0), ("default", -1, 1)):
+        capi.setQuESTTuning("wave_wg_per_cu", per)
+        capi.setQuESTTuning("wave_dynamic", dyn)
+        reg = qa.Register(env, n)
+        reg.init_plus()
+        capi.resetQuESTStats()
+        random_layered(n, 10, seed=n).apply(reg)
+        outs[name] = reg.to_numpy()
+        assert capi.getQuESTStats()["wavePasses"] > 0
+        reg.close()
+    capi.setQuESTTuning("wave_wg_per_cu", -1)
+    capi.setQuESTTuning("wave_dynamic", 1)
+    assert np.array_equal(outs["one"], outs["default"])
+    assert np.array_equal(outs["one"], outs["static"])
+    assert abs(np.vdot(outs["default"], outs["default"]).real - 1) < 1e-12
+
+
 XFRAME = r'''
 import os, sys
 import numpy as np

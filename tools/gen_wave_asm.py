@@ -31,7 +31,7 @@ Device records (host side: src/hip/backend_hip.hip, WaveLaunchDev / WaveOpDev):
            + 88   u64 ldGroupByte[16]   + 216 u64 stGroupByte[16]
            + 344  u32 ldLaneByte[64]    + 600 u32 stLaneByte[64]
            + 1024 u64 ldWaveByte[16]    + 1152 u64 stWaveByte[16]
-           + 1280 u64 debugBuf
+           + 1280 u64 debugBuf       + 1288 u32 tileCounter[8]
            pos[b] for b >= 12 sits in bits 8.. of pos[b - 12]
            + 2048 WaveOpDev ops[]  (96 B: i32 handler, u32 cReg, u32 cLane,
                   u32 aux, u64 ctrlOut, u64 pad, f64 m[8] / f32 m[16])
@@ -45,6 +45,9 @@ import sys
 
 KINDS = ["M2", "M2R", "M2RI", "ANTI", "SWAP"]
 LD_WAVE, ST_WAVE, DEBUG_BUF, OPS_OFF = 1024, 1152, 1280, 2048   # launch-record offsets (see above)
+# dynamic tile claims of looping grids: u32 counters (one per launch sharing
+# the record, kernel argument bits 5-7), zeroed by the host's upload
+TILE_CNT = 1288
 import os as _os
 # cache policy of the state stream (non-temporal by default); WAVE_LD_POLICY /
 # WAVE_ST_POLICY override for experiments, e.g. "" or " sc1"
@@ -321,7 +324,7 @@ def schedule(body):
 
 
 class Gen:
-    def __init__(self, R, dbuf, W, P=2, debug=False, nomem=False, lean=False):
+    def __init__(self, R, dbuf, W, P=2, debug=False, nomem=False, lean=False, pfa=0, pfl=0):
         self.lean = lean        # 80 VGPRs / half outboxes: three 8-wave workgroups per CU
         self.nomem = nomem      # experiment: no state loads / stores (compute time alone)
         self.debug = debug
@@ -367,6 +370,19 @@ class Gen:
             self.CL = self.C0             # lane-gate coefficients in C0 / C1 (scratch: vTmp)
             self.CLA = self.C0
             self.nvgpr = D + (nt + 2) * P + 4
+        # dynamic tile claims (looping grids): the claimed counter value (wave 0,
+        # lane 0) and the LDS address of the slot it is published through
+        self.vNext, self.vSlot = self.nvgpr, self.nvgpr + 1
+        self.nvgpr += 2
+        # next-tile prefetch of looping grids (pf_paths): PFA of a tile's
+        # 16-byte loads per lane land in AGPRs, PFL in this wave's LDS area
+        # (vPF: its address for this lane); the rest load at the tile's end
+        self.PFA, self.PFL = pfa, pfl
+        self.PF = 0 if (dbuf or nomem) else pfa + pfl
+        if self.PF:
+            assert self.PF <= 2 * (self.NS * P // 4)
+            self.vPF = self.nvgpr
+            self.nvgpr += 1
         self.handlers = {}
         # real lane bits below this transpose with a slot through LDS
         # (gen_tr_lds), the others by DPP / v_permlane*_swap
@@ -1428,7 +1444,11 @@ class Gen:
         e("s_add_u32 s16, s16, s98")
         self.label(".Lmap_done")
         e("s_mov_b32 s17, 0")
+        e(f"v_mov_b32_e32 v{self.vSlot}, {self.dyn_lds()}")
         e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        if self.PF:
+            e("s_bitcmp1_b32 s100, 4")
+            e("s_cbranch_scc1 .Lpf_start")
         if self.dbuf:
             # Software pipeline: while the ops run on tile i (registers A), tile
             # i+1 is already loading into registers B; at the top of iteration
@@ -1485,7 +1505,9 @@ class Gen:
             self.wave_bytes(LD_WAVE, 34)
             self.groups("ld", 88, vldb, NG, 0, 96)
             e("s_waitcnt vmcnt(0)")
+            self.dyn_claim()
         # ---- op loop: prefetch op 0, then every op starts through next_op()
+        self.label(".Lops_begin")
         e("s_mov_b64 s[94:95], s[10:11]")
         e("s_load_dwordx16 s[36:51], s[94:95], 0x0")
         self.label(".Lnext")
@@ -1494,6 +1516,9 @@ class Gen:
         self.label("wh_OPS_DONE")     # the sentinel record's handler
         self.handlers[LAYOUT["done"]] = "wh_OPS_DONE"
         e("s_waitcnt lgkmcnt(0)")      # the prefetch past the last op writes s[36:59]
+        if self.PF:
+            e("s_bitcmp1_b32 s100, 4")
+            e("s_cbranch_scc1 .Lpf_end")
         if self.W:
             # store barrier (launch + 20, bit 30; set by the host for passes
             # whose store moves wave bits to other positions and that have no
@@ -1508,6 +1533,8 @@ class Gen:
             self.label(".Lst_nobar")
         self.wave_bytes(ST_WAVE, 34)
         self.groups("st", 216, vstb, NG, 0, 96)
+        if not self.dbuf:
+            self.dyn_next(0 if self.nomem else 2 * NG)
         e("s_add_u32 s16, s16, s14")
         e("s_addc_u32 s17, s17, s15")
         if self.dbuf:
@@ -1515,6 +1542,8 @@ class Gen:
         e("s_branch .Ltile_loop")
         self.label(".Ldone")
         e("s_endpgm")
+        if self.PF:
+            self.pf_paths(NG)
         # ---- handlers
         for kind in KINDS:
             for s in range(R):
@@ -1563,6 +1592,275 @@ class Gen:
         L.append(".Lfunc_end0:")
         L.append("\t.size\tqa_wave_tile, .Lfunc_end0-qa_wave_tile")
         self.descriptor()
+
+    def dyn_lds(self):
+        """LDS byte address of the two tile-claim slots (after the outboxes)."""
+        return self.NW * self.OUTBOX if (self.W or self.tr_lds) else 0
+
+    def pf_lds(self):
+        """LDS byte address of the prefetch areas (after the claim slots)."""
+        return self.dyn_lds() + 16
+
+    def pf_items(self, NG):
+        """The tile's 16-byte loads per lane in groups() order: (jj, array
+        SGPR pair, first VGPR); the last PF of them are prefetched."""
+        out = []
+        for jj in range(NG):
+            out.append((jj, 4, 4 * jj))
+            out.append((jj, 6, self.P * self.NS + 4 * jj))
+        return out
+
+    def pf_addr(self, Q, arr, bpair, jj):
+        """Descriptor base of one 16-byte load / store: array + tile base
+        (+ this wave's offset) + the group's offset (loaded to s[52:83] by
+        half: groups 8h..8h+7 at s[52 + 16 slot]...)."""
+        e = self.e
+        g = 52 + 2 * (jj % 8) if self.pf_half_slot[jj // 8] == 0 else 68 + 2 * (jj % 8)
+        e(f"s_add_u32 s{Q}, s{arr}, s{bpair}")
+        e(f"s_addc_u32 s{Q + 1}, s{arr + 1}, s{bpair + 1}")
+        e(f"s_add_u32 s{Q}, s{Q}, s{g}")
+        e(f"s_addc_u32 s{Q + 1}, s{Q + 1}, s{g + 1}")
+
+    def pf_vm(self, n=1):
+        """Keep at most 63 vector-memory instructions in flight (the counter's
+        range): a wait before an issue that could exceed it."""
+        if self.pf_ub + n > 63:
+            self.e(f"s_waitcnt vmcnt({63 - n})")
+            self.pf_ub = 63 - n
+        self.pf_ub += n
+
+    def pf_paths(self, NG):
+        """Looping grids with a next-tile prefetch (kernel argument bit 4 of a
+        kernel generated with --pfa / --pfl).  Each workgroup runs tile t while
+        tile t' = its next is already loading: at the top of tile t the last
+        PF of t''s 16-byte loads per lane go to AGPRs / this wave's LDS area,
+        the ops run, then t's stores go out -- each of the other groups'
+        stores directly followed by the load of t''s group into the same
+        registers -- and after one wait the prefetched groups are copied into
+        place.  Claims: the first two tiles are the workgroup id and id +
+        grid, later ones 2 grid + (counter value claimed one tile ahead)."""
+        e = self.e
+        items = self.pf_items(NG)
+        n = len(items)
+        P_from = n - self.PF
+        pitems = [(k, items[k]) for k in range(P_from, n)]
+        ditems = [(k, items[k]) for k in range(P_from)]
+        # P item -> ("a", AGPR quad index) or ("l", LDS slot index)
+        where = {}
+        for i, (k, _) in enumerate(pitems):
+            where[k] = ("a", i) if i < self.PFA else ("l", i - self.PFA)
+        quads = (36, 40, 44, 48)
+
+        def set_desc():
+            for Q in quads:
+                e(f"s_mov_b32 s{Q + 2}, -1")
+                e(f"s_mov_b32 s{Q + 3}, 0x20000")
+
+        def load_offsets(st_half, ld_half):
+            # st / ld group offsets of half h into s[52:67] / s[68:83]
+            self.pf_half_slot = {}
+            if st_half is not None:
+                e(f"s_load_dwordx16 s[52:67], s[8:9], {216 + 64 * st_half}")
+            if ld_half is not None:
+                e(f"s_load_dwordx16 s[68:83], s[8:9], {88 + 64 * ld_half}")
+            e("s_waitcnt lgkmcnt(0)")
+
+        # ---- start: the first tile loads directly
+        self.label(".Lpf_start")
+        e("s_add_u32 s0, s16, s14")                     # t' = first tile + grid
+        e(f"s_mul_i32 s1, s3, {self.PFL * 1024}")
+        e(f"s_add_u32 s1, s1, {self.pf_lds()}")          # this wave's LDS prefetch area
+        e(f"v_lshlrev_b32_e32 v{self.vPF}, 4, v{self.vLane}")
+        e(f"v_add_u32_e32 v{self.vPF}, s1, v{self.vPF}")
+        self.tile_check("s[16:17]", ".Ldone")
+        self.base_of("s[16:17]", 32)
+        self.wave_bytes(LD_WAVE, 34)
+        self.groups("ld", 88, self.vLdB, NG, 0, 96)
+        e("s_waitcnt vmcnt(0)")
+        # ---- top of tile t: claim t'' and prefetch t''s last PF loads
+        self.label(".Lpf_top")
+        self.base_of("s[16:17]", 32)                    # this tile: ctrlOut tests and stores
+        e("s_sub_u32 s98, s0, s12")
+        e("s_subb_u32 s99, 0, s13")
+        e("s_cbranch_scc0 .Lops_begin")                 # no t': nothing to claim or prefetch
+        self.pf_ub = self.PF                            # the previous tile's prefetched groups' stores
+        self.pf_vm()
+        self.dyn_claim()
+        e("s_mov_b32 s84, s0")
+        e("s_mov_b32 s85, 0")
+        self.base_of("s[84:85]", 84)
+        self.wave_bytes(LD_WAVE, 86)                    # s[96:97]: t''s bytes + this wave's
+        halves = sorted({jj // 8 for _, (jj, _, _) in pitems})
+        set_desc()
+        q = 0
+        for h in halves:
+            load_offsets(None, h)
+            self.pf_half_slot = {h: 1}
+            for k, (jj, arr, vb) in pitems:
+                if jj // 8 != h:
+                    continue
+                Q = quads[q % 4]
+                q += 1
+                self.pf_addr(Q, arr, 96, jj)
+                self.pf_vm()
+                kind, i = where[k]
+                if kind == "a":
+                    e(f"buffer_load_dwordx4 a[{4 * i}:{4 * i + 3}], v{self.vLdB}, s[{Q}:{Q + 3}], 0 offen{LD_POLICY}")
+                else:
+                    e(f"s_add_u32 m0, s1, {1024 * i}")
+                    e(f"buffer_load_dwordx4 v{self.vLdB}, s[{Q}:{Q + 3}], 0 offen{LD_POLICY} lds")
+        e("s_branch .Lops_begin")
+        # ---- end of tile t
+        self.label(".Lpf_end")
+        if self.W:
+            e("s_load_dword s96, s[8:9], 0x14")
+            e("s_waitcnt lgkmcnt(0)")
+            e("s_bitcmp1_b32 s96, 30")
+            e("s_cbranch_scc0 .Lpf_nobar")
+            e("s_barrier")
+            self.label(".Lpf_nobar")
+        e("s_waitcnt vmcnt(0)")                         # t''s prefetch and the claim have landed
+        self.pf_ub = 0
+        e("s_sub_u32 s98, s0, s12")
+        e("s_subb_u32 s99, 0, s13")
+        e("s_cbranch_scc1 .Lpf_more")
+        # the workgroup's last tile: plain stores
+        self.wave_bytes(ST_WAVE, 34)
+        self.groups("st", 216, self.vStB, NG, 0, 96)
+        e("s_endpgm")
+        self.label(".Lpf_more")
+        e("s_mov_b32 s84, s0")
+        e("s_mov_b32 s85, 0")
+        self.base_of("s[84:85]", 84)
+        e("s_lshl_b32 s98, s3, 3")
+        e(f"s_add_u32 s98, s98, {LD_WAVE}")
+        e("s_load_dwordx2 s[88:89], s[8:9], s98 offset:0x0")
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_add_u32 s88, s88, s86")                    # s[88:89]: t''s bytes + this wave's
+        e("s_addc_u32 s89, s89, s87")
+        self.wave_bytes(ST_WAVE, 34)                    # s[96:97]: t's store bytes + this wave's
+        set_desc()
+        q = 0
+        # the other groups: store, then t''s load into the same registers
+        for h in sorted({jj // 8 for _, (jj, _, _) in ditems}):
+            load_offsets(h, h)
+            self.pf_half_slot = {h: 0}
+            for k, (jj, arr, vb) in ditems:
+                if jj // 8 != h:
+                    continue
+                Q = quads[q % 4]
+                q += 1
+                self.pf_addr(Q, arr, 96, jj)
+                self.pf_vm()
+                e(f"buffer_store_dwordx4 v[{vb}:{vb + 3}], v{self.vStB}, s[{Q}:{Q + 3}], 0 offen{ST_POLICY}")
+                Q = quads[q % 4]
+                q += 1
+                self.pf_half_slot = {h: 1}
+                self.pf_addr(Q, arr, 88, jj)
+                self.pf_half_slot = {h: 0}
+                self.pf_vm()
+                e(f"buffer_load_dwordx4 v[{vb}:{vb + 3}], v{self.vLdB}, s[{Q}:{Q + 3}], 0 offen{LD_POLICY}")
+        # the prefetched groups: stores only (the last VMEM instructions)
+        for h in halves:
+            load_offsets(h, None)
+            self.pf_half_slot = {h: 0}
+            for k, (jj, arr, vb) in pitems:
+                if jj // 8 != h:
+                    continue
+                Q = quads[q % 4]
+                q += 1
+                self.pf_addr(Q, arr, 96, jj)
+                self.pf_vm()
+                e(f"buffer_store_dwordx4 v[{vb}:{vb + 3}], v{self.vStB}, s[{Q}:{Q + 3}], 0 offen{ST_POLICY}")
+        e(f"s_waitcnt vmcnt({self.PF})")                # t''s direct loads (and everything older) landed
+        # publish the claim (wave 0), take it after the barrier (which also
+        # orders the LDS prefetch for the reads below)
+        e("s_cmp_eq_u32 s3, 0")
+        e("s_cbranch_scc0 .Lpf_bar")
+        e("s_mov_b64 s[98:99], exec")
+        e("s_mov_b64 exec, 1")
+        e(f"ds_write_b32 v{self.vSlot}, v{self.vNext}")
+        e("s_mov_b64 exec, s[98:99]")
+        self.label(".Lpf_bar")
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_barrier")
+        e(f"ds_read_b32 v{self.vNext}, v{self.vSlot}")
+        e(f"v_xor_b32_e32 v{self.vSlot}, 4, v{self.vSlot}")
+        e("s_nop 1")
+        for k, (jj, arr, vb) in pitems:
+            kind, i = where[k]
+            if kind == "a":
+                for x in range(4):
+                    e(f"v_accvgpr_read_b32 v{vb + x}, a{4 * i + x}")
+            else:
+                e(f"ds_read_b128 v[{vb}:{vb + 3}], v{self.vPF} offset:{1024 * i}")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"v_readfirstlane_b32 s94, v{self.vNext}")
+        e("s_nop 4")
+        e("s_mov_b32 s16, s0")
+        e("s_mov_b32 s17, 0")
+        e("s_lshl_b32 s0, s14, 1")
+        e("s_add_u32 s0, s0, s94")                      # t'' = 2 grid + its claim
+        e("s_branch .Lpf_top")
+
+    def dyn_claim(self):
+        """Looping grids with dynamic claims (kernel argument bit 4): wave 0's
+        lane 0 claims the workgroup's next tile now -- an atomic add on the
+        launch's counter (bits 5-7 pick it) that returns during the ops.  A
+        static stride would give each workgroup tiles with the same low index
+        bits, and with them the same out-of-tile controls: some workgroups
+        would run every controlled op and others none (persistent grids ran
+        18 % slower than one-tile grids on compute alone)."""
+        e = self.e
+        self.dyn_label = getattr(self, "dyn_label", 0) + 1
+        skip = f".Ldyn_claim_{self.dyn_label}"
+        e("s_bitcmp1_b32 s100, 4")
+        e(f"s_cbranch_scc0 {skip}")
+        e("s_cmp_eq_u32 s3, 0")
+        e(f"s_cbranch_scc0 {skip}")
+        e("s_bfe_u32 s96, s100, 0x30005")             # counter index (bits 5-7)
+        e("s_lshl_b32 s96, s96, 2")
+        e(f"s_add_u32 s96, s96, {TILE_CNT}")
+        e("s_add_u32 s96, s8, s96")
+        e("s_addc_u32 s97, s9, 0")
+        e(f"v_mov_b32_e32 v{self.vNext}, 1")
+        e("s_mov_b64 s[98:99], exec")
+        e("s_mov_b64 exec, 1")
+        # (vLane is 0 in lane 0: the counter's own address)
+        e(f"global_atomic_add v{self.vNext}, v{self.vLane}, v{self.vNext}, s[96:97] sc0")
+        e("s_mov_b64 exec, s[98:99]")
+        self.label(skip)
+
+    def dyn_next(self, newer):
+        """End of a tile with dynamic claims: wave 0 publishes its claim
+        through LDS (two slots used alternately, so a wave that runs a tile
+        ahead cannot overwrite a slot another wave has yet to read), every
+        wave of the workgroup takes it after a barrier and continues with tile
+        waveStride + claim.  `newer`: VMEM instructions issued after the claim
+        (the tile's stores), which its wait leaves in flight."""
+        e = self.e
+        static, bar = ".Ldyn_static", ".Ldyn_bar"
+        e("s_bitcmp1_b32 s100, 4")
+        e(f"s_cbranch_scc0 {static}")
+        e("s_cmp_eq_u32 s3, 0")
+        e(f"s_cbranch_scc0 {bar}")
+        e(f"s_waitcnt vmcnt({newer})")
+        e("s_mov_b64 s[98:99], exec")
+        e("s_mov_b64 exec, 1")
+        e(f"ds_write_b32 v{self.vSlot}, v{self.vNext}")
+        e("s_mov_b64 exec, s[98:99]")
+        self.label(bar)
+        e("s_waitcnt lgkmcnt(0)")
+        e("s_barrier")
+        e(f"ds_read_b32 v{self.vNext}, v{self.vSlot}")
+        e(f"v_xor_b32_e32 v{self.vSlot}, 4, v{self.vSlot}")
+        e("s_waitcnt lgkmcnt(0)")
+        e(f"v_readfirstlane_b32 s16, v{self.vNext}")
+        e("s_nop 4")                          # VALU-written SGPR read by SALU
+        e("s_add_u32 s16, s16, s14")
+        e("s_mov_b32 s17, 0")
+        e("s_branch .Ltile_loop")
+        self.label(static)
 
     def tile_check(self, tile, done):
         """Branch to `done` unless tile < numTiles (s[12:13])."""
@@ -1707,11 +2005,17 @@ class Gen:
     def descriptor(self):
         nv = self.nvgpr
         nv8 = (nv + 7) // 8 * 8
+        accum, nagpr = nv8, 0
+        if self.PF and self.PFA:
+            # unified register file: AGPRs after the architectural VGPRs
+            accum = (nv + 3) // 4 * 4
+            nagpr = 4 * self.PFA
+            nv8 = (accum + nagpr + 7) // 8 * 8
         L = self.lines
         L.append("\t.section\t.rodata,\"a\",@progbits")
         L.append("\t.p2align\t6, 0x0")
         L.append("\t.amdhsa_kernel qa_wave_tile")
-        lds = self.NW * self.OUTBOX if (self.W or self.tr_lds) else 0
+        lds = self.pf_lds() + (self.NW * self.PFL * 1024 if self.PF else 0)   # outboxes, claim slots, prefetch
         for k, v in [("group_segment_fixed_size", lds), ("private_segment_fixed_size", 0), ("kernarg_size", 32),
                      ("user_sgpr_count", 2), ("user_sgpr_dispatch_ptr", 0), ("user_sgpr_queue_ptr", 0),
                      ("user_sgpr_kernarg_segment_ptr", 1), ("user_sgpr_dispatch_id", 0),
@@ -1720,7 +2024,7 @@ class Gen:
                      ("enable_private_segment", 0), ("system_sgpr_workgroup_id_x", 1),
                      ("system_sgpr_workgroup_id_y", 0), ("system_sgpr_workgroup_id_z", 0),
                      ("system_sgpr_workgroup_info", 0), ("system_vgpr_workitem_id", 0),
-                     ("next_free_vgpr", nv8), ("next_free_sgpr", 102), ("accum_offset", nv8),
+                     ("next_free_vgpr", nv8), ("next_free_sgpr", 102), ("accum_offset", accum),
                      ("reserve_vcc", 1), ("float_round_mode_32", 0), ("float_round_mode_16_64", 0),
                      ("float_denorm_mode_32", 3), ("float_denorm_mode_16_64", 3), ("dx10_clamp", 1),
                      ("ieee_mode", 1), ("fp16_overflow", 0), ("tg_split", 0)]:
@@ -1732,7 +2036,7 @@ class Gen:
         L.append("\t.amdgpu_metadata")
         L.append(f"""---
 amdhsa.kernels:
-  - .agpr_count:     0
+  - .agpr_count:     {nagpr}
     .args:
       - .address_space:  global
         .offset:         0
@@ -1811,6 +2115,8 @@ def main():
     ap.add_argument("--setprio", action="store_true",
                     help="experiment: raise the wave priority while issuing a tile's loads / stores")
     ap.add_argument("--lean", type=int, default=0, help="1: 80-VGPR layout, half outboxes (3 workgroups per CU)")
+    ap.add_argument("--pfa", type=int, default=0, help="next-tile prefetch: 16-byte loads per lane into AGPRs")
+    ap.add_argument("--pfl", type=int, default=0, help="next-tile prefetch: 16-byte loads per lane into LDS")
     ap.add_argument("--out", required=True)
     ap.add_argument("--obj")
     ap.add_argument("--hsaco")
@@ -1820,11 +2126,13 @@ def main():
         # a tile has <= 4 waves (otherwise too few workgroups fit a CU)
         dbuf = args.dbuf if args.dbuf >= 0 else (args.slots <= 4 and args.wbits <= 2)
         set_layout(args.slots)
-        g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug, args.nomem, bool(args.lean))
+        g = Gen(args.slots, dbuf, args.wbits, 2 if args.prec == 2 else 1, args.debug, args.nomem, bool(args.lean),
+                args.pfa, args.pfl)
         g.setprio = args.setprio
         g.kernel()
         with open(args.out, "w") as f:
             f.write("// GENERATED by tools/gen_wave_asm.py -- do not edit\n")
+            f.write(f"// wave_prefetch {g.PF}\n")
             f.write("\n".join(g.lines) + "\n")
         # handler names per table index, for the embed step
         with open(args.out + ".handlers", "w") as f:
@@ -1842,8 +2150,17 @@ def main():
         f.write("// GENERATED by tools/gen_wave_asm.py embed -- do not edit\n")
         f.write(f"static const int kWaveImageSlots = {args.slots};\n")
         f.write(f"static const int kWaveImageWBits = {args.wbits};\n")
-        vg = re.search(r"amdhsa_next_free_vgpr (\d+)", open(args.out.replace("wave_image.inc", "wave_kernel.s")).read())
+        src = open(args.out.replace("wave_image.inc", "wave_kernel.s")).read()
+        vg = re.search(r"amdhsa_next_free_vgpr (\d+)", src)
         f.write(f"static const int kWaveImageVgprs = {vg.group(1)};\n")
+        lds = int(re.search(r"amdhsa_group_segment_fixed_size (\d+)", src).group(1))
+        pf = int(re.search(r"// wave_prefetch (\d+)", src).group(1))
+        # resident workgroups per CU (512 registers per SIMD lane, 160 KiB LDS;
+        # a workgroup of 2^wbits waves puts 2^wbits / 4 of them on each SIMD)
+        per_simd = 512 // int(vg.group(1))
+        wg = min(per_simd * 4 // (1 << args.wbits), (160 * 1024) // max(1, lds))
+        f.write(f"static const int kWaveImagePrefetch = {pf};\n")
+        f.write(f"static const int kWaveImageWgPerCU = {max(1, wg)};\n")
         set_layout(args.slots)
         f.write(f"static const int kWaveImagePrec = {args.prec};\n")
         for k in ("slot", "d2s", "d2l", "tr", "diag", "trw", "lane", "slot2", "ph", "ch", "slotL", "slot2L", "d2sL", "swk", "check"):
