@@ -33,6 +33,9 @@ Besides the headline, a single-GPU run adds (outside the timed region, ~10 s):
   * ``window1_s_per_gate``: the seed-7 circuit flushed after every layer
     (the scheduler sees one layer at a time, as in a program that reads the
     state between layers);
+  * ``fused_sweep``: the same axis on the fused path -- the five seeds'
+    layered circuits (3 warm-up + 10 timed layers) at n = 20, 22, ..., 32 and
+    34 (one seed, 20 layers): s/gate, passes and s/gate / 2^(n - 30);
   * ``q34``: 34 qubits (256 GiB, the largest state one MI355X holds): unfused
     H on targets 0 / 17 / 33 and a 6-layer random layered circuit;
   * ``density17``: a 17-qubit density matrix (2^34 amplitudes): damping,
@@ -58,6 +61,7 @@ BASELINE_S_PER_OP = 3783.9266747315614 / 667  # fork's estimate, tutorial_exampl
 
 
 DEFAULT_SEEDS = "7,11,12,13,17"   # 7: the rounds-1..4 headline; 11-13, 17 never used for tuning
+FUSED_SWEEP_SEEDS = (7, 11, 12, 13, 17)
 
 
 def split_layers(circ, n, layers):
@@ -80,7 +84,7 @@ def main():
     ap.add_argument("--seeds", default=DEFAULT_SEEDS, help="comma-separated circuit seeds, one window each")
     ap.add_argument("--seed", type=int, default=None, help="a single circuit seed (overrides --seeds)")
     ap.add_argument("--no-extras", action="store_true", help="skip every extra (single-GPU runs only)")
-    ap.add_argument("--extras", default="window1,fork30,sweep,rotate29,q34,density17,fp32",
+    ap.add_argument("--extras", default="window1,fork30,sweep,rotate29,fused_sweep,q34,density17,fp32",
                     help="comma-separated extras of a single-GPU run")
     ap.add_argument("--allow-transport", action="store_true", help="accept a non-RCCL transport with N > 1")
     args = ap.parse_args()
@@ -254,7 +258,7 @@ def run_extras(qa, reg, n, layer_gates, args, seed):
     docstring); closes the bench register before the 256 GiB ones."""
     from quest_amd.models import fork_circuit
     from quest_amd.models.circuits import Circuit
-    from quest_amd.utils.bench_workloads import run_density17, run_q34, run_rotate29
+    from quest_amd.utils.bench_workloads import run_density17, run_fused_sweep, run_q34, run_rotate29
 
     todo = set(args.extras.split(","))
     out = {}
@@ -333,6 +337,9 @@ def run_extras(qa, reg, n, layer_gates, args, seed):
     reg.close()
     if qa.capi.binding().prec == 2:
         res = {}
+        if "fused_sweep" in todo:
+            guarded("fused_sweep", lambda: (run_fused_sweep(env, res, seeds=FUSED_SWEEP_SEEDS),
+                                            out.__setitem__("fused_sweep", res["fused_sweep"])))
         if "q34" in todo:
             guarded("q34", lambda: (run_q34(env, res), out.__setitem__("q34", res["q34"])))
         if "density17" in todo:

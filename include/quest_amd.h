@@ -148,6 +148,7 @@ typedef struct QuESTStats {
     long long overlappedSwaps;  /* swaps run on a stream of their own, next to gate passes (QUEST_SWAP_OVERLAP) */
     long long overlappedPasses; /* passes started on the part of the chunk a swap in flight leaves in place */
     long long layoutAligns;   /* swaps / chunk restores before which this rank moved its local qubits to rank 0's positions */
+    long long placementProbes; /* re / im placements measured by the allocation probe (HIP; 1 when a remembered one was taken) */
 } QuESTStats;
 void getQuESTStats(QuESTStats* stats);
 void resetQuESTStats(void);

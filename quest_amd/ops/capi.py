@@ -83,7 +83,7 @@ class _Binding:
                          "verifiedFlushes", "wavePasses", "waveOps", "waveTransposes", "relabels",
                          "globalDiags", "flushes", "marginalPasses", "waveShadowChecks",
                          "waveShadowMismatches", "permutedOps", "relayouts", "restoreRounds", "swapMicros",
-                         "overlappedSwaps", "overlappedPasses", "layoutAligns")]
+                         "overlappedSwaps", "overlappedPasses", "layoutAligns", "placementProbes")]
 
         self.Complex, self.ComplexMatrix2, self.Vector = Complex, ComplexMatrix2, Vector
         self.ComplexArray, self.QASMLogger, self.Qureg = ComplexArray, QASMLogger, Qureg

@@ -215,6 +215,65 @@ def run_q34(env, res, n=34):
     r.close()
 
 
+def run_fused_sweep(env, res, seeds=(7, 11, 12, 13, 17), sizes=(20, 22, 24, 26, 28, 30, 32, 34), layers=10,
+                    warmup=3, layers34=20):
+    """The metric's "vs #qubits" axis on the fused path: the headline's
+    seeded random layered circuits (one window of `layers` layers per seed
+    after `warmup` untimed ones, |+>^n) at every size, one register per size
+    re-initialised per seed.  Per size: s/gate (total time / total gates over
+    the seeds), passes, and s/gate / 2^(n - 30) -- the per-amplitude rate
+    against the 30-qubit one (1.0 = the same cost per byte).  34 qubits
+    (256 GiB) runs `layers34` layers.  Below 23 qubits a wave pass has fewer
+    tiles (2^(n - 13)) than the 768 resident workgroups of the chip, so
+    small states pay occupancy and launch latency, not bandwidth."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+    from quest_amd.models.circuits import Circuit
+
+    def split(circ, n, nl):
+        out, i = [], 0
+        for layer in range(nl):
+            cnt = n + len(range(layer % 2, n - 1, 2))
+            out.append(circ.gates[i:i + cnt])
+            i += cnt
+        return out
+
+    rows = []
+    for n in sizes:
+        nl = layers34 if n >= 34 else layers
+        r = qa.Register(env, n)
+        tot_t, tot_g, tot_p = 0.0, 0, 0
+        per_seed = []
+        for sd in seeds:
+            lg = split(random_layered(n, warmup + nl, seed=sd), n, warmup + nl)
+            r.init_plus()
+            for w in range(warmup):
+                Circuit(n, lg[w]).apply(r)
+            r.sync()
+            p0 = qa.capi.getQuESTStats()["passes"]
+            t0 = time.perf_counter()
+            g = 0
+            for w in range(warmup, warmup + nl):
+                Circuit(n, lg[w]).apply(r)
+                g += len(lg[w])
+            r.sync()
+            dt = time.perf_counter() - t0
+            p = qa.capi.getQuESTStats()["passes"] - p0
+            tot_t, tot_g, tot_p = tot_t + dt, tot_g + g, tot_p + p
+            per_seed.append(round(dt / g, 9))
+            if n >= 34:
+                break   # one seed at 256 GiB (its window alone is ~1.5 s)
+        spg = tot_t / tot_g
+        rows.append({"n": n, "layers": nl, "seeds": len(per_seed), "s_per_gate": spg, "passes": tot_p,
+                     "passes_per_layer": tot_p / (nl * len(per_seed)), "per_seed_s_per_gate": per_seed,
+                     "scaled_to_30": spg / 2.0 ** (n - 30), "norm_error": abs(r.total_prob() - 1)})
+        r.close()
+    ref = next((x["scaled_to_30"] for x in rows if x["n"] == 30), None)
+    for x in rows:
+        x["per_byte_vs_30q"] = x["scaled_to_30"] / ref if ref else None
+    res["fused_sweep"] = rows
+
+
 def run_density17(env, res, n=17):
     import quest_amd as qa
 

@@ -1201,6 +1201,7 @@ void getQuESTStats(QuESTStats* s) {
     s->overlappedSwaps = stats().overlappedSwaps;
     s->overlappedPasses = stats().overlappedPasses;
     s->layoutAligns = stats().layoutAligns;
+    s->placementProbes = stats().placementProbes;
 }
 
 void resetQuESTStats(void) {

@@ -41,6 +41,21 @@ enum class OpKind : int {
     DensChan2 = 3,  // two-qubit dephase/depolarise superoperator, see below
 };
 
+// Rank predicates of distributed registers (router issue): an op controlled by
+// a rank qubit, a phase on one and a collapse of one used to be queued only on
+// the ranks where they apply -- so the ranks' planners saw different op lists
+// and could relabel local qubits differently (round 5 patched that with a
+// layout broadcast before every swap).  Now every rank queues the SAME op,
+// tagged in ctrl bits 48..62 (above every local position, at least two bits:
+// never fused into a two-qubit block) -- an out-of-tile control to every
+// planner, so all ranks plan the same passes -- and the rank's verdict sits in
+// QuregImpl::rankSkip[tag].  Backends resolve tags where they execute ops
+// (resolveRankTag): the tag bits cleared where the op runs; left in place
+// where it does not, where no local index matches them (the op is skipped).
+constexpr int kRankTagShift = 48;
+constexpr int kRankTagCount = 1 << 14;                     // tag ids 1 .. 16383 (bits 48..61) + marker bit 62
+constexpr unsigned long long kRankTagMask = 0x7fffull << kRankTagShift;
+
 // DensChan2 acts on the 16 elements spanned by t = {row q1, row q2, col q1, col q2}.
 // With a = bit(t0) + 2 bit(t1) and b = bit(t2) + 2 bit(t3):
 //   a != b : x *= m[0].re                          (off-diagonal dephasing)
@@ -78,7 +93,8 @@ struct QuregImpl {
     i64 lastUse[64];
     std::vector<Op> pending;  // ops queued for fusion (backend-owned semantics)
     std::vector<Op> lpending; // distributed registers: ops in LOGICAL qubits awaiting routing
-    bool jointAlloc = false;  // HIP: re and im share one allocation (freed through re)
+    bool jointAlloc = false;  // HIP: re and im share one allocation (freed through allocBase)
+    void* allocBase = nullptr;  // HIP: that allocation (re may start inside it)
     void* be = nullptr;       // backend-private state
     // Router-level change counter of the LOGICAL state (bumped identically on
     // every rank by every op / overwrite) and the one-qubit marginals cached
@@ -107,6 +123,10 @@ struct QuregImpl {
     // its flush; -1 none): the backend can split the passes that avoid them
     int swapVictims[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
     int nSwapVictims = 0;
+    // rank predicates (kRankTagMask): this rank's verdict per tag id (1: the
+    // op does not apply here), tags handed out round robin
+    std::vector<unsigned char> rankSkip;
+    int rankTagNext = 0;
     bool permIdentity() const {
         for (int i = 0; i < nSV; i++)
             if (l2p[i] != i) return false;
@@ -115,6 +135,25 @@ struct QuregImpl {
 };
 
 constexpr unsigned kQuregMagic = 0x51A3D355u;
+
+// The rank-tag verdicts of the register being flushed (set by the backends'
+// flush for its duration; RankSkipScope) and the resolution of a predicate
+// mask against them: tag bits cleared when the op applies on this rank.
+const unsigned char*& rankSkipTable();
+[[noreturn]] void rankTagFatal();
+inline u64 resolveRankTag(u64 m) {
+    if (!(m & kRankTagMask)) return m;
+    const unsigned char* s = rankSkipTable();
+    if (!s) rankTagFatal();
+    return s[(m >> kRankTagShift) & (kRankTagCount - 1)] ? m : (m & ~kRankTagMask);
+}
+struct RankSkipScope {
+    const unsigned char* prev;
+    explicit RankSkipScope(const QuregImpl& q) : prev(rankSkipTable()) {
+        rankSkipTable() = q.rankSkip.empty() ? nullptr : q.rankSkip.data();
+    }
+    ~RankSkipScope() { rankSkipTable() = prev; }
+};
 
 QuregImpl* impl(const Qureg& q);
 

@@ -32,6 +32,16 @@ void verifyFlush(int qubits, size_t ops, size_t passes, double maxDiff) {
     exit(EXIT_FAILURE);
 }
 
+const unsigned char*& rankSkipTable() {
+    static thread_local const unsigned char* t = nullptr;
+    return t;
+}
+
+void rankTagFatal() {
+    fprintf(stderr, "QuEST: an op carries a rank tag outside a register flush\n");
+    exit(EXIT_FAILURE);
+}
+
 QuregImpl* impl(const Qureg& q) {
     QuregImpl* p = reinterpret_cast<QuregImpl*>(q.qasmLog);
     if (!p || p->magic != kQuregMagic) {
@@ -71,6 +81,25 @@ void ensureXBuf(int peers, i64 amps, bool withSend = true) {
 inline int chunkBit(const QuregImpl& q, int phys) { return (q.chunkId >> (phys - q.L)) & 1; }
 
 inline bool distributed(const QuregImpl& q) { return q.L < q.nSV; }
+
+
+// Rank predicates as tags (core.hpp kRankTagMask; QUEST_RANK_TAGS=0: the
+// round-5 behaviour, ops queued only where they apply + layout alignment).
+bool rankTagsOn(const QuregImpl& q) {
+    static const bool on = !getenv("QUEST_RANK_TAGS") || atoi(getenv("QUEST_RANK_TAGS")) != 0;
+    return on && distributed(q) && q.L < kRankTagShift;
+}
+
+// A fresh tag whose verdict on this rank is `skip` (the same tag id on every
+// rank: tags are handed out in op order, which is the same everywhere).  A tag
+// is reused after kRankTagCount - 1 newer ones, long after the backend queue
+// (at most 1024 ops) has run the op that carried it.
+u64 rankTag(QuregImpl& q, bool skip) {
+    if (q.rankSkip.empty()) q.rankSkip.assign((size_t)kRankTagCount, 1);
+    q.rankTagNext = q.rankTagNext % (kRankTagCount - 1) + 1;
+    q.rankSkip[(size_t)q.rankTagNext] = skip ? 1 : 0;
+    return (1ull << 62) | ((u64)q.rankTagNext << kRankTagShift);
+}
 
 // Rank holding logical chunk c (see QuregImpl::chunkRank).
 inline int rankOf(const QuregImpl& q, int c) { return q.chunkRank.empty() ? c : q.chunkRank[(size_t)c]; }
@@ -159,6 +188,20 @@ void swapOrder(const QuregImpl& q, const int* gposIn, const int* lposIn, int k, 
 void alignLayouts(QuregImpl& q) {
     static const bool on = !getenv("QUEST_ALIGN_LAYOUTS") || atoi(getenv("QUEST_ALIGN_LAYOUTS")) != 0;   // (0: study)
     if (!on || !distributed(q)) return;
+    if (rankTagsOn(q)) {
+        // Round 6: every rank plans the same op list (rank predicates are
+        // tags, core.hpp), so the layouts agree by construction.  Checked with
+        // a 64-bit hash through the bootstrap's host rendezvous -- no device
+        // sync, unlike the layout broadcast -- and aligned below only if they
+        // do not (counted in layoutAligns: the tests assert it stays 0).
+        u64 h = 1469598103934665603ull;
+        for (int p = 0; p < q.L; p++) h = (h ^ (u64)(unsigned)q.p2l[p]) * 1099511628211ull;
+        std::vector<u64> all((size_t)rt().numRanks);
+        boot::allgather(rt().rank, rt().numRanks, &h, all.data(), sizeof h);
+        bool same = true;
+        for (u64 x : all) same = same && x == all[0];
+        if (same) return;
+    }
     int ref[64];
     for (int p = 0; p < 64; p++) ref[p] = p < q.nSV ? q.p2l[p] : -1;
     comm::bcastHost(ref, sizeof ref, 0);
@@ -357,25 +400,6 @@ u64 logicalTargets(const Op& op) {
     return m;
 }
 
-// Logical op -> physical op for the backend.  Controls (and the phase mask
-// of a diagonal op) on rank bits are decided per rank: either this rank's
-// whole chunk satisfies them (dropped from the mask) or none of it does (the
-// op is skipped here) -- no communication.
-void issue(QuregImpl& q, const Op& lop) {
-    Op op = lop;
-    op.ctrl = 0;
-    for (int i = 0; i < lop.nt; i++) op.t[i] = q.l2p[lop.t[i]];
-    for (u64 c = lop.ctrl; c; c &= c - 1) {
-        const int p = q.l2p[__builtin_ctzll(c)];
-        if (p >= q.L) {
-            if (!chunkBit(q, p)) return;
-        } else {
-            op.ctrl |= 1ull << p;
-        }
-    }
-    enqueue(q, op);
-}
-
 // Per-rank scalar (times a local-control mask): Diag op over the chunk.
 void scaleChunk(QuregImpl& q, u64 localCtrl, cplx s) {
     if (isOne(s)) return;
@@ -387,20 +411,72 @@ void scaleChunk(QuregImpl& q, u64 localCtrl, cplx s) {
     enqueue(q, op);
 }
 
+// Logical op -> physical op for the backend.  Controls (and the phase mask
+// of a diagonal op) on rank bits are decided per rank: either this rank's
+// whole chunk satisfies them (dropped from the mask) or none of it does (the
+// op is skipped here) -- no communication.
+void issue(QuregImpl& q, const Op& lop) {
+    Op op = lop;
+    op.ctrl = 0;
+    for (int i = 0; i < lop.nt; i++) op.t[i] = q.l2p[lop.t[i]];
+    bool rankCtl = false, skip = false;
+    for (u64 c = lop.ctrl; c; c &= c - 1) {
+        const int p = q.l2p[__builtin_ctzll(c)];
+        if (p >= q.L) {
+            rankCtl = true;
+            skip = skip || !chunkBit(q, p);
+        } else {
+            op.ctrl |= 1ull << p;
+        }
+    }
+    if (rankCtl) {
+        if (!rankTagsOn(q)) {
+            if (skip) return;
+        } else {
+            op.ctrl |= rankTag(q, skip);
+        }
+    }
+    enqueue(q, op);
+}
+
+// A diagonal whose value depends on this rank's chunk: v[b] on the chunks
+// whose rank bits `bitsOf` take the value b (b = 0, 1), on amplitudes with the
+// local controls; `skipCtl`: the rank controls of the op fail here.  With rank
+// tags every rank queues both values (the same ops everywhere); else the
+// round-5 per-rank scaling.
+void rankDiagPair(QuregImpl& q, u64 localCtrl, bool skipCtl, int b, cplx v0, cplx v1) {
+    if (!rankTagsOn(q)) {
+        if (!skipCtl) scaleChunk(q, localCtrl, b ? v1 : v0);
+        return;
+    }
+    for (int v = 0; v < 2; v++) {
+        const cplx s = v ? v1 : v0;
+        if (isOne(s)) continue;   // (the same decision on every rank)
+        Op op;
+        op.kind = OpKind::Diag;
+        op.nt = 0;
+        op.ctrl = localCtrl | rankTag(q, skipCtl || b != v);
+        op.m[0] = s;
+        enqueue(q, op);
+    }
+}
+
 // Diagonal one-qubit gate on a rank qubit: scale by m[b][b].
 void issueRankDiag(QuregImpl& q, const Op& lop) {
     const int b = chunkBit(q, q.l2p[lop.t[0]]);
     u64 ctrl = 0;
+    bool skip = false;
     for (u64 c = lop.ctrl; c; c &= c - 1) {
         const int p = q.l2p[__builtin_ctzll(c)];
         if (p >= q.L) {
-            if (!chunkBit(q, p)) return;
+            skip = skip || !chunkBit(q, p);
         } else {
             ctrl |= 1ull << p;
         }
     }
+    if (skip && !rankTagsOn(q)) return;
     stats().globalDiags++;
-    scaleChunk(q, ctrl, lop.m[b ? 3 : 0]);
+    rankDiagPair(q, ctrl, skip, b, lop.m[0], lop.m[3]);
 }
 
 // Anti-diagonal one-qubit gate on a rank qubit, controls on rank qubits
@@ -416,10 +492,11 @@ void issueRankAnti(QuregImpl& q, const Op& lop) {
         if ((c & cm) == cm) nr[(size_t)(c ^ tb)] = q.chunkRank[(size_t)c];
     q.chunkRank.swap(nr);
     stats().relabels++;
-    if ((q.chunkId & cm) != cm) return;
-    q.chunkId ^= tb;
+    const bool skip = (q.chunkId & cm) != cm;
+    if (skip && !rankTagsOn(q)) return;
+    if (!skip) q.chunkId ^= tb;
     const int b = (q.chunkId & tb) ? 1 : 0;
-    scaleChunk(q, 0, lop.m[b ? 2 : 1]);
+    rankDiagPair(q, 0, skip, b, lop.m[1], lop.m[2]);
 }
 
 // Exchange this rank's whole chunk with `peer`'s (every pair of a round calls
@@ -847,11 +924,16 @@ void collapse(QuregImpl& q, int qubit, int outcome, real renorm) {
     flushLogical(q);
     int p = q.l2p[qubit];
     if (p >= q.L) {
+        const cplx keep = {renorm, 0}, drop = {0, 0};
+        if (rankTagsOn(q)) {   // (the same two ops on every rank)
+            rankDiagPair(q, 0, false, chunkBit(q, p), outcome ? drop : keep, outcome ? keep : drop);
+            return;
+        }
         Op op;
         op.kind = OpKind::Diag;
         op.nt = 0;
         op.ctrl = 0;
-        op.m[0] = {chunkBit(q, p) == outcome ? renorm : (real)0, 0};
+        op.m[0] = chunkBit(q, p) == outcome ? keep : drop;
         enqueue(q, op);
         return;
     }
@@ -876,6 +958,10 @@ void densCollapse(QuregImpl& q, int qubit, int outcome, real prob) {
     bool rGlobal = r >= q.L, cGlobal = c >= q.L;
     if (rGlobal && cGlobal) {
         bool keepChunk = chunkBit(q, r) == outcome && chunkBit(q, c) == outcome;
+        if (rankTagsOn(q)) {   // (the same two ops on every rank)
+            rankDiagPair(q, 0, false, keepChunk ? 1 : 0, {0, 0}, {s, 0});
+            return;
+        }
         Op op;
         op.kind = OpKind::Diag;
         op.nt = 0;
@@ -886,6 +972,27 @@ void densCollapse(QuregImpl& q, int qubit, int outcome, real prob) {
     if (rGlobal || cGlobal) {
         int gpos = rGlobal ? r : c, lpos = rGlobal ? c : r;
         Op op;
+        if (rankTagsOn(q)) {
+            // (the same two ops on every rank: the projector where the
+            // chunk's bit is the outcome, zero elsewhere)
+            const bool match = chunkBit(q, gpos) == outcome;
+            op.kind = OpKind::Mat2;
+            op.nt = 1;
+            op.t[0] = lpos;
+            op.ctrl = rankTag(q, !match);
+            op.m[0] = {outcome == 0 ? s : (real)0, 0};
+            op.m[1] = {0, 0};
+            op.m[2] = {0, 0};
+            op.m[3] = {outcome == 1 ? s : (real)0, 0};
+            enqueue(q, op);
+            Op z;
+            z.kind = OpKind::Diag;
+            z.nt = 0;
+            z.ctrl = rankTag(q, match);
+            z.m[0] = {0, 0};
+            enqueue(q, z);
+            return;
+        }
         if (chunkBit(q, gpos) != outcome) {
             op.kind = OpKind::Diag;
             op.nt = 0;

@@ -104,6 +104,7 @@ struct Stats {
     long long restoreRounds = 0;  // concurrent rounds of whole-chunk exchanges restoring chunk placement
     long long overlappedSwaps = 0;   // swaps issued on their own stream (be::swapOverlapBegin)
     long long overlappedPasses = 0;  // passes started on the part a swap in flight leaves in place
+    long long placementProbes = 0;   // re / im placements measured by the allocation probe
 };
 Stats& stats();
 

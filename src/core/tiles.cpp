@@ -54,6 +54,7 @@ void emitPass(const std::vector<Op>& ops, int b, int e, u64 tmask, int L, int k,
             else
                 t.ctrlOut |= 1ull << bit;
         }
+        t.ctrlOut |= op.ctrl & kRankTagMask;   // a rank predicate: out of every tile (core.hpp)
         int nm = op.kind == OpKind::Mat2 ? 4 : op.kind == OpKind::Mat4 ? 16 : op.kind == OpKind::Diag ? 1 : 3;
         for (int j = 0; j < nm; j++) {
             t.m[2 * j] = op.m[j].re;
@@ -253,6 +254,7 @@ int support(const Op& op, int q[2]) {
     };
     if (op.kind == OpKind::DensChan2) return -1;
     if (op.kind == OpKind::Mat4 && op.ctrl) return -1;
+    if (op.ctrl & kRankTagMask) return -1;   // rank-predicated ops stay single (core.hpp)
     for (int i = 0; i < op.nt; i++)
         if (!add(op.t[i])) return -1;
     for (u64 c = op.ctrl; c; c &= c - 1)

@@ -1531,7 +1531,7 @@ bool planWavePass(const TilePass& ps, const TileOp* ops, int nOps, WaveProgram& 
     // a real diagonal factor that is not a unit phase (those have cheap kinds)
     auto foldable = [&](int x) {
         const real* m = ops[x].m;
-        return foldOn && m[1] == 0 && m[0] != 0 && std::fabs((double)m[0]) != 1;
+        return foldOn && m[1] == 0 && m[0] != 0 && std::fabs((double)m[0]) != 1 && !(ops[x].ctrlOut & kRankTagMask);
     };
     for (int i = 0; i < nOps; i++) {
         if (cframeOn) {

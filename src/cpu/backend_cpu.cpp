@@ -312,10 +312,21 @@ void runTilePass(real* re, real* im, int L, const TileProgram& prog, const TileP
     }
 }
 
-void runProgram(real* re, real* im, int L, const TileProgram& prog, bool wave = false) {
+void runProgram(real* re, real* im, int L, const TileProgram& prog0, bool wave = false) {
+    // rank predicates (core.hpp): the ops are planned as queued, identically on
+    // every rank, then resolved against this rank's verdicts for execution
+    bool tagged = false;
+    for (const TileOp& op : prog0.ops) tagged = tagged || (op.ctrlOut & kRankTagMask);
+    TileProgram resolved;
+    if (tagged) {
+        resolved = prog0;
+        for (TileOp& op : resolved.ops) op.ctrlOut = resolveRankTag(op.ctrlOut);
+    }
+    const TileProgram& prog = tagged ? resolved : prog0;
     for (const TilePass& ps : prog.passes) {
         WaveProgram wp;
-        if (wave && planWavePass(ps, prog.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, wp)) {
+        if (wave && planWavePass(ps, prog0.ops.data() + ps.opBegin, ps.opEnd - ps.opBegin, wp)) {
+            for (WaveOp& w : wp.ops) w.ctrlOut = resolveRankTag(w.ctrlOut);
             emulateWavePass(re, im, L, wp, wp.passes[0]);
             stats().wavePasses++;
         } else {
@@ -454,6 +465,7 @@ void flush(QuregImpl& q) { flushImpl(q, false); }
 namespace {
 void flushImpl(QuregImpl& q, bool front) {
     if (q.pending.empty()) return;
+    const RankSkipScope rankScope(q);
     TileProgram prog;
     std::vector<Op> raw;
     if (rt().verify) raw = q.pending;

@@ -317,6 +317,9 @@ bool launchDirectOp(real* re, real* im, int L, const Op& op, bool launch) {
     const long long N = 1ll << L;
     if (N < (long long)VN * 2048) return false;  // small states: one tile pass is as good
     if (op.kind != OpKind::Mat2 && op.kind != OpKind::Diag) return false;
+    // a rank predicate still tagged after resolution: the op does not apply on
+    // this rank (core.hpp kRankTagMask) -- nothing to launch
+    if (op.ctrl & kRankTagMask) return true;
     // directLowToTile = 1: targets / controls inside a 128-byte line go to
     // the LDS tile pass instead of the in-vector and lane-shuffle kernels.
     if (tuning().directLowToTile) {

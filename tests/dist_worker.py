@@ -21,6 +21,13 @@ def main():
     res = SCENARIOS[name](env)
     res["_ranks"] = env.num_ranks
     res["_transport"] = qa.capi.getQuESTTransport()
+    # every rank's own counters (a rank other than 0 is the one that would
+    # have aligned its layout)
+    import json
+
+    st = qa.capi.getQuESTStats()
+    with open(f"{out}.rank{env.rank}.json", "w") as f:
+        json.dump({k: int(st[k]) for k in ("layoutAligns", "swaps", "passes")}, f)
     if env.rank == 0:
         import numpy as np
 

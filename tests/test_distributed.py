@@ -111,18 +111,26 @@ def test_wave_relabelling_with_rank_swaps(env, tmp_path, ranks):
 
 def test_rank_controlled_ops_keep_layouts_aligned(env, tmp_path, monkeypatch):
     """24 qubits on 4 ranks (22 local, wave-planned by the host emulation): the
-    bench's seed-13 circuit has CNOTs controlled by rank qubits, which run only
-    on the ranks whose bit is 1, so the ranks' planners relabel differently.
-    Every swap first brings the ranks' local layouts to rank 0's (router
-    alignLayouts); without that (QUEST_ALIGN_LAYOUTS=0) the swaps cut their
-    parts at different logical qubits: marginals off by 0.06 with the norm
-    intact -- and an in-place IPC swap on the GPU lost norm."""
+    bench's seed-13 circuit has CNOTs controlled by rank qubits.  Round 5 ran
+    them only on the ranks whose bit is 1 (QUEST_RANK_TAGS=0), so the ranks'
+    planners relabelled differently and every swap first had to bring the
+    local layouts to rank 0's (router alignLayouts; without it the swaps cut
+    their parts at different logical qubits: marginals off by 0.06 with the
+    norm intact).  Round 6 queues them on every rank as rank-tagged ops
+    (core.hpp kRankTagMask): the plans agree by construction and no rank ever
+    aligns (tests/test_fuzz_dist.py: the plans themselves compared, and the
+    control without tags diverging)."""
+    import json
+
     monkeypatch.setenv("RCR_QUBITS", "24")
     want = _single("rank_controlled_relabel", env)
     got = _multi("rank_controlled_relabel", 4, tmp_path, QUEST_CPU_PLANNER="3", RCR_QUBITS="24")
     for k in ("probs", "amps", "norm"):
         np.testing.assert_allclose(np.asarray(got[k]), np.asarray(want[k]), rtol=0, atol=1e-11, err_msg=k)
     assert int(got["_swaps"]) > 0
+    out = str(tmp_path / "rank_controlled_relabel_4.npz")
+    aligns = [json.load(open(f"{out}.rank{r}.json"))["layoutAligns"] for r in range(4)]
+    assert max(aligns) == 0, aligns
 
 
 @pytest.mark.parametrize("name", ["random_ops_statevector", "calculations", "layered_wave_relabel"])
