@@ -253,12 +253,23 @@ void done(const int* peers, int n, hipStream_t producer) {
         int a = 1, b = 0;
         sock::sendrecv(peers[i], &a, &b, sizeof a);
     }
-    // Unmap the peers' state arrays now that our swap kernels are done with
-    // them: a mapping kept until the peer's next token would pin a register
-    // the peer may destroy meanwhile, and a destroy-then-create of a register
-    // of the same size could then run out of device memory.
-    static const bool keep = getenv("QUEST_IPC_KEEP_STATE") && atoi(getenv("QUEST_IPC_KEEP_STATE"));   // (study)
-    for (size_t i = 0; i < g_imported.size() && !keep;) {
+    // Round 6: the peers' state mappings stay open for the next swap (round 5
+    // closed them here and re-opened them with every swap -- the call the
+    // driver now and then refuses with several ranks on one device).  They
+    // are released when a register is destroyed (forget, below): destroying a
+    // register is collective, so every rank drops its mappings of the peers'
+    // states at the same point and the peer's memory is really free for the
+    // next allocation.  QUEST_IPC_CLOSE_STATE=1: the round-5 behaviour.
+    static const bool close = getenv("QUEST_IPC_CLOSE_STATE") && atoi(getenv("QUEST_IPC_CLOSE_STATE"));
+    if (close) releaseStateMappings();
+}
+
+void releaseStateMappings() {
+    bool any = false;
+    for (const Imported& m : g_imported) any = any || m.state;
+    if (!any) return;
+    QA_HIP_CHECK(hipDeviceSynchronize());   // (no kernel of ours still reads them)
+    for (size_t i = 0; i < g_imported.size();) {
         if (g_imported[i].state) {
             QA_HIP_CHECK(hipIpcCloseMemHandle(g_imported[i].ptr));
             g_imported.erase(g_imported.begin() + (long)i);
@@ -269,6 +280,7 @@ void done(const int* peers, int n, hipStream_t producer) {
 }
 
 void forget(const void* p) {
+    releaseStateMappings();
     const char* c = static_cast<const char*>(p);
     for (size_t i = 0; i < g_exported.size(); i++)
         if (c >= g_exported[i].base && c < g_exported[i].base + g_exported[i].size) {

@@ -55,6 +55,10 @@ void done(const int* peers, int n, hipStream_t producer);
 // A comm buffer is about to be freed: forget its handle (a later allocation
 // at the same address gets a new id, so peers re-open it).
 void forget(const void* p);
+// Close every mapping of a peer's state array (mapArrays): before a register
+// is freed (forget) -- destroying one is collective, so all ranks release
+// their mappings of each other's states there.
+void releaseStateMappings();
 std::string describe();
 
 }  // namespace ipc

@@ -837,9 +837,19 @@ bool footprintCheck(int nSV, int numRanks, std::string& report) {
              nSV, numRanks, m.state / G, 2.0 * 2 * np * bytes / G, 2 * np, bytes / 1048576.0, g, m.scratch / G,
              m.total / G, tot / G, f0 / G, f1 / G, known ? "" : " (unknown)");
     report = std::string(head) + r;
-    // the plan is an upper bound: its maximum can come from a k < g term or
-    // the chunk restore, and direct / in-place swaps allocate less
-    return ok && (long long)(2 * 2 * np * bytes) <= m.exchange;
+    // The plan's exchange term is the largest of the k = 1 .. g all-to-alls'
+    // and the chunk restore's buffer sets (direct / in-place swaps allocate
+    // less): recomputed here from the slice rule, it must equal the plan
+    // exactly, and the k = g buffers just allocated must fit in it.
+    long long bound = 0;
+    for (int k = 1; k <= g; k++) {
+        i64 sk = (rt().exchangeSliceBytes >> (k - 1)) / (i64)(2 * sizeof(real));
+        sk = std::min(std::max<i64>(sk, 16), ((i64)1 << L) >> k);
+        bound = std::max(bound, 2ll * 2 * ((1ll << k) - 1) * (long long)sizeof(real) * 2 * sk);
+    }
+    const i64 sr = std::min<i64>((i64)1 << L, std::max<i64>(rt().exchangeSliceBytes / (i64)(2 * sizeof(real)), 1));
+    bound = std::max(bound, 2ll * 2 * (long long)sizeof(real) * 2 * sr);
+    return ok && bound == m.exchange && (long long)(2 * 2 * np * bytes) <= m.exchange;
 }
 
 void create(QuregImpl& q, int nSV, bool density) {

@@ -730,7 +730,53 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             }
             return sc;
         };
-        double bestScore = score(best);
+        // Rollout scoring (QUEST_PLAN_ROLLOUT=1, experiment): a candidate
+        // pass is judged by how many passes the plain greedy planner (with
+        // first-use relabelling) then needs for the rest of the queue --
+        // fewer first, more ops taken now on ties
+        static const int rolloutEnv = getenv("QUEST_PLAN_ROLLOUT") ? atoi(getenv("QUEST_PLAN_ROLLOUT")) : 0;
+        const int rollout = hooks && hooks->rollout >= 0 ? hooks->rollout : rolloutEnv;
+        auto tileFor = [&](u64 high) {
+            TilePass ps;
+            u64 q = high | low;
+            for (int bit = 0; popcount64(q) < k && bit < L; bit++)
+                if (!((avoid >> bit) & 1)) q |= 1ull << bit;
+            for (int bit = 0; popcount64(q) < k && bit < L; bit++) q |= 1ull << bit;
+            int m = 0;
+            for (int bit = 0; bit < L; bit++)
+                if ((q >> bit) & 1) ps.pos[m++] = bit;
+            ps.k = m;
+            return ps;
+        };
+        auto rolloutPasses = [&](const std::vector<int>& cand, u64 candHigh) {
+            const std::vector<Op> keepOps(ops.begin() + first, ops.end());
+            const int keepFirst = first;
+            std::vector<int> marked(cand);
+            for (int i : cand) done[i] = 1;
+            int passes = 0;
+            u64 high = candHigh;
+            std::vector<int> pick;
+            while (true) {
+                while (first < n && done[first]) first++;
+                if (first >= n) break;
+                if (relabelFrom >= 0 && rollout >= 1) {
+                    int pi[64];
+                    if (proposePerm(ops, done, first, relabelFrom, c, tileFor(high), 0, pi)) applyPerm(ops, done, first, pi);
+                }
+                high = scan(0, pick);
+                if (pick.empty()) break;
+                for (int i : pick) {
+                    done[i] = 1;
+                    marked.push_back(i);
+                }
+                passes++;
+            }
+            for (int i : marked) done[i] = 0;
+            first = keepFirst;
+            std::copy(keepOps.begin(), keepOps.end(), ops.begin() + first);
+            return passes;
+        };
+        double bestScore = rollout ? -1e6 * rolloutPasses(best, bestHigh) + (double)best.size() : score(best);
         static const int maxSeedsEnv = [] {
             const char* e = getenv("QUEST_PLAN_SEEDS");
             return e ? atoi(e) : 24;
@@ -749,7 +795,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             if (dup || nTried == 16) continue;
             tried[nTried++] = h;
             const u64 hh = scan(h, take);
-            const double sc = score(take);
+            const double sc = rollout ? -1e6 * rolloutPasses(take, hh) + (double)take.size() : score(take);
             if (sc > bestScore) {
                 best.swap(take);
                 bestHigh = hh;

@@ -186,6 +186,10 @@ struct PlanHooks {
     // swap about to run, router planSwap): passes whose ops do not target
     // them then leave them out, so the swap can overlap those passes
     u64 avoidMask = 0;
+    // rollout scoring of candidate passes (-1: QUEST_PLAN_ROLLOUT, default 0;
+    // 1: the greedy plan of the rest of the queue with first-use relabelling
+    // counts the passes a candidate leaves) -- a strategy of the search
+    int rollout = -1;
 };
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,

@@ -673,6 +673,7 @@ struct WaveStrategy {
     int cframe;    // conditional exchange frame: 1 as configured, 0 off
     int commute;   // class-aware commutation in the scheduler (t_planCommute): -1 as configured, 0 off, 1 on
     double mem = 0;  // trimming bound in modeled cycles (0: waveCostHooks')
+    int roll = 0;    // rollout scoring of candidate passes (PlanHooks::rollout)
 };
 // 0 is the configured default (cost = -1, cframe = -1: waveCostHooks and the
 // environment as they are); the 8th is the round-3 planner (no compute-aware
@@ -682,7 +683,10 @@ const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1, -1}, {1, 1, 0, -1, 1, -1}
                                     {0, 1, 0, 0.5, 1, -1},  {0, 0, 0, -1, 0, -1},  {0, -1, 0, -1, -1, 1},
                                     {1, 1, 0, -1, 1, 1},    {0, 0, 0, -1, 1, 1},   {1, 0, 0, -1, 1, 1},
                                     {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1},  {0, 1, 0, -1, 1, -1, 15000},
-                                    {0, 1, 0, -1, 1, -1, 17500}};
+                                    {0, 1, 0, -1, 1, -1, 17500},
+                                    // round 6: rollout-scored candidates
+                                    {0, 1, 0, -1, 1, -1, 0, 1}, {1, 1, 0, -1, 1, -1, 0, 1}, {0, 0, 0, -1, 1, -1, 0, 1},
+                                    {-1, 1, 0, -1, 1, -1, 0, 1}};
 constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
 // strategies the search tries (QUEST_PLAN_STRATEGIES, default all 16: with
 // the commutation and one-fewer-resident-position variants the five bench
@@ -695,7 +699,11 @@ constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0])
 int searchStrategies() {
     static const int n = [] {
         const char* e = getenv("QUEST_PLAN_STRATEGIES");
-        const int v = e ? atoi(e) : kNumStrategies;
+        // (round 6: the four rollout strategies after the first 16 are opt-in,
+        // QUEST_PLAN_STRATEGIES=20 -- bench seeds unchanged at 80 passes, fresh
+        // seeds 21-30 166 -> 163, at ten times the host time per strategy:
+        // profiles/r6/rollout_strategies.txt)
+        const int v = e ? atoi(e) : 16;
         return v < 1 ? 1 : v > kNumStrategies ? kNumStrategies : v;
     }();
     return n;
@@ -707,6 +715,7 @@ void strategyHooks(const WaveStrategy& st, PlanHooks& h) {
     const double M = costed.memCost > 0 ? costed.memCost : 12800.0;
     h.seeds = st.seeds;
     h.lookahead = st.look;
+    h.rollout = st.roll;
     if (st.cost < 0) {   // as configured
         h.passCost = nullptr;
         h.memCost = 0;
