@@ -698,6 +698,52 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         }
         if (kept.size() < v.size() && !kept.empty()) v.swap(kept);
     };
+    // Rollout scoring (QUEST_PLAN_ROLLOUT=1, experiment): a candidate
+    // pass is judged by how many passes the plain greedy planner (with
+    // first-use relabelling) then needs for the rest of the queue --
+    // fewer first, more ops taken now on ties
+    static const int rolloutEnv = getenv("QUEST_PLAN_ROLLOUT") ? atoi(getenv("QUEST_PLAN_ROLLOUT")) : 0;
+    const int rollout = hooks && hooks->rollout >= 0 ? hooks->rollout : rolloutEnv;
+    auto tileFor = [&](u64 high) {
+        TilePass ps;
+        u64 q = high | low;
+        for (int bit = 0; popcount64(q) < k && bit < L; bit++)
+            if (!((avoid >> bit) & 1)) q |= 1ull << bit;
+        for (int bit = 0; popcount64(q) < k && bit < L; bit++) q |= 1ull << bit;
+        int m = 0;
+        for (int bit = 0; bit < L; bit++)
+            if ((q >> bit) & 1) ps.pos[m++] = bit;
+        ps.k = m;
+        return ps;
+    };
+    auto rolloutPasses = [&](const std::vector<int>& cand, u64 candHigh) {
+        const std::vector<Op> keepOps(ops.begin() + first, ops.end());
+        const int keepFirst = first;
+        std::vector<int> marked(cand);
+        for (int i : cand) done[i] = 1;
+        int passes = 0;
+        u64 high = candHigh;
+        std::vector<int> pick;
+        while (true) {
+            while (first < n && done[first]) first++;
+            if (first >= n) break;
+            if (relabelFrom >= 0 && rollout >= 1) {
+                int pi[64];
+                if (proposePerm(ops, done, first, relabelFrom, c, tileFor(high), 0, pi)) applyPerm(ops, done, first, pi);
+            }
+            high = scan(0, pick);
+            if (pick.empty()) break;
+            for (int i : pick) {
+                done[i] = 1;
+                marked.push_back(i);
+            }
+            passes++;
+        }
+        for (int i : marked) done[i] = 0;
+        first = keepFirst;
+        std::copy(keepOps.begin(), keepOps.end(), ops.begin() + first);
+        return passes;
+    };
     while ((int)order.size() < n) {
         while (done[first]) first++;
         const int begin = (int)order.size();
@@ -729,52 +775,6 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 sc += beta * (double)nextTake.size();
             }
             return sc;
-        };
-        // Rollout scoring (QUEST_PLAN_ROLLOUT=1, experiment): a candidate
-        // pass is judged by how many passes the plain greedy planner (with
-        // first-use relabelling) then needs for the rest of the queue --
-        // fewer first, more ops taken now on ties
-        static const int rolloutEnv = getenv("QUEST_PLAN_ROLLOUT") ? atoi(getenv("QUEST_PLAN_ROLLOUT")) : 0;
-        const int rollout = hooks && hooks->rollout >= 0 ? hooks->rollout : rolloutEnv;
-        auto tileFor = [&](u64 high) {
-            TilePass ps;
-            u64 q = high | low;
-            for (int bit = 0; popcount64(q) < k && bit < L; bit++)
-                if (!((avoid >> bit) & 1)) q |= 1ull << bit;
-            for (int bit = 0; popcount64(q) < k && bit < L; bit++) q |= 1ull << bit;
-            int m = 0;
-            for (int bit = 0; bit < L; bit++)
-                if ((q >> bit) & 1) ps.pos[m++] = bit;
-            ps.k = m;
-            return ps;
-        };
-        auto rolloutPasses = [&](const std::vector<int>& cand, u64 candHigh) {
-            const std::vector<Op> keepOps(ops.begin() + first, ops.end());
-            const int keepFirst = first;
-            std::vector<int> marked(cand);
-            for (int i : cand) done[i] = 1;
-            int passes = 0;
-            u64 high = candHigh;
-            std::vector<int> pick;
-            while (true) {
-                while (first < n && done[first]) first++;
-                if (first >= n) break;
-                if (relabelFrom >= 0 && rollout >= 1) {
-                    int pi[64];
-                    if (proposePerm(ops, done, first, relabelFrom, c, tileFor(high), 0, pi)) applyPerm(ops, done, first, pi);
-                }
-                high = scan(0, pick);
-                if (pick.empty()) break;
-                for (int i : pick) {
-                    done[i] = 1;
-                    marked.push_back(i);
-                }
-                passes++;
-            }
-            for (int i : marked) done[i] = 0;
-            first = keepFirst;
-            std::copy(keepOps.begin(), keepOps.end(), ops.begin() + first);
-            return passes;
         };
         double bestScore = rollout ? -1e6 * rolloutPasses(best, bestHigh) + (double)best.size() : score(best);
         static const int maxSeedsEnv = [] {
@@ -837,6 +837,22 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             int choice = -1;
             if (forced >= 0) {
                 if (forced < 2 && has[forced]) choice = forced;
+            } else if (rollout >= 2) {
+                // (rollout 2: the store permutation judged by the passes the
+                // rest of the queue then needs, next-pass ops on ties)
+                static const std::vector<int> none;
+                auto judge = [&]() { return -1e6 * rolloutPasses(none, bestHigh) + (double)nextPassOps(); };
+                double bestV = judge();
+                for (int m = 0; m < 2; m++) {
+                    if (!has[m] || (m == 1 && has[0] && !memcmp(pis[0], pis[1], sizeof pis[0]))) continue;
+                    applyPerm(ops, done, first, pis[m]);
+                    const double v = judge();
+                    applyPerm(ops, done, first, pis[m]);   // involution: undo
+                    if (v > bestV) {
+                        bestV = v;
+                        choice = m;
+                    }
+                }
             } else {
                 size_t bestNext = nextPassOps();
                 for (int m = 0; m < 2; m++) {

@@ -685,8 +685,8 @@ const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1, -1}, {1, 1, 0, -1, 1, -1}
                                     {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1},  {0, 1, 0, -1, 1, -1, 15000},
                                     {0, 1, 0, -1, 1, -1, 17500},
                                     // round 6: rollout-scored candidates
-                                    {0, 1, 0, -1, 1, -1, 0, 1}, {1, 1, 0, -1, 1, -1, 0, 1}, {0, 0, 0, -1, 1, -1, 0, 1},
-                                    {-1, 1, 0, -1, 1, -1, 0, 1}};
+                                    {0, 1, 0, -1, 1, -1, 0, 1}, {1, 1, 0, -1, 1, -1, 0, 2}, {0, 0, 0, -1, 1, -1, 0, 1},
+                                    {0, 1, 0, -1, 1, -1, 0, 2}};
 constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0]);
 // strategies the search tries (QUEST_PLAN_STRATEGIES, default all 16: with
 // the commutation and one-fewer-resident-position variants the five bench
