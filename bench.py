@@ -147,22 +147,25 @@ def main():
         r.sync()
         st = qa.capi.getQuESTStats()
         marks.append((time.perf_counter() - ts, g, st["passes"], st["swaps"], st["bytesExchanged"],
-                      st["swapMicros"]))
+                      st["swapMicros"], st["overlappedPasses"]))
         gates += g
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     barrier()
     elapsed = allreduce_max(time.perf_counter() - t0)
     stats = qa.capi.getQuESTStats()
-    seed_rows, prev = [], (0, 0, 0, 0)
-    for sd, (dt, g, p, sw, by, us) in zip(seeds, marks):
+    seed_rows, prev = [], (0, 0, 0, 0, 0)
+    for sd, (dt, g, p, sw, by, us, ov) in zip(seeds, marks):
         dt = allreduce_max(dt)
         row = {"seed": sd, "s_per_gate": dt / max(g, 1), "window_ms": 1e3 * dt, "passes": p - prev[0]}
         if world > 1:
             swap_ms = allreduce_max((us - prev[3]) * 1e-3)
             row.update({"swaps": sw - prev[1], "swap_bytes_per_rank": by - prev[2], "swap_ms": swap_ms,
-                        "swap_share": swap_ms / (1e3 * dt) if dt > 0 else None})
-        prev = (p, sw, by, us)
+                        "swap_share": swap_ms / (1e3 * dt) if dt > 0 else None,
+                        # wave passes launched while a swap was in flight (on the
+                        # part it keeps, or range by range as ranges landed)
+                        "overlapped_passes": int(allreduce_max(float(ov - prev[4])))})
+        prev = (p, sw, by, us, ov)
         seed_rows.append(row)
 
     reg = regs[0]
@@ -200,7 +203,8 @@ def main():
                  "swap_share": swap_ms / (1e3 * elapsed) if elapsed > 0 else None,
                  "swap_GBps_per_rank": (stats["bytesExchanged"] / (swap_ms * 1e-3) / 1e9) if swap_ms > 0 else None,
                  # swaps before which some rank had to bring its local qubits to rank 0's positions
-                 "layout_aligns_max": int(allreduce_max(float(stats["layoutAligns"])))}
+                 "layout_aligns_max": int(allreduce_max(float(stats["layoutAligns"]))),
+                 "overlapped_swaps": stats["overlappedSwaps"], "overlapped_passes": stats["overlappedPasses"]}
     result = {
         "metric": "single-qubit-gate time (s) vs #qubits, fp64 state-vector; 1/2/4/8-GPU scaling",
         "value": s_per_gate,

@@ -124,6 +124,16 @@ void swapOverlapEnd(QuregImpl& q);
 // it keeps only once the swap has been issued, next to the transfer.  False
 // if this backend does not split (nothing changed).
 bool preSwap(QuregImpl& q, const int* lpos, int k, int myG);
+// Receive-side overlap (round 6; the swapped positions may be tile bits): the
+// exchange's slices arrive in the order of the chunk's top local positions
+// other than lpos -- rangePos[0..b), b <= 3 -- and swapRangeLanded(q, v) is
+// called once every slice of range v (rangePos bits = v) has been unpacked.
+// Passes of q launched while the swap is in flight whose tiles avoid rangePos
+// then run range by range, each range once it has landed, next to the
+// transfer of the later ranges; flushes meanwhile keep rangePos out of tile
+// padding.  Call after swapOverlapBegin returned true, before any slice.
+void swapRanges(QuregImpl& q, const int* rangePos, int b);
+void swapRangeLanded(QuregImpl& q, int v);
 // Local positions the ops queued for q target, plus the low positions every
 // planned tile holds: swap victims outside them are never a tile bit of the
 // passes that flush plans.

@@ -127,6 +127,11 @@ struct QuregImpl {
     // op does not apply here), tags handed out round robin
     std::vector<unsigned char> rankSkip;
     int rankTagNext = 0;
+    // local positions the first pass planned after a swap keeps out of its
+    // tile, targets included (router multiSwap: the swap's receive ranges,
+    // so that pass can run range by range as they land); consumed by the
+    // next flush that plans a pass
+    u64 firstPassAvoid = 0;
     bool permIdentity() const {
         for (int i = 0; i < nSV; i++)
             if (l2p[i] != i) return false;

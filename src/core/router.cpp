@@ -329,6 +329,37 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn0, int k) {
         const i64 nSlices = (partSize + slice - 1) / slice;
         if (direct)
             for (int b = 0; b < 2; b++) xs[b].resize((size_t)(2 * np));
+        // Receive-side overlap (round 6, be::swapRanges): the slices run in
+        // the natural order of the part, i.e. by the chunk's top local
+        // positions other than the swapped ones -- the first post-swap passes
+        // (whose tiles hold the incoming qubits) run range by range as the
+        // ranges land, next to the transfer of the later ones.
+        int nRange = 0, rangePos[3];
+        i64 perRange = nSlices;
+        // (QUEST_SWAP_RANGES_STUDY=1: the ranges' planning constraint on any
+        // backend, for host plan studies of its pass count)
+        static const bool study = getenv("QUEST_SWAP_RANGES_STUDY") && atoi(getenv("QUEST_SWAP_RANGES_STUDY")) != 0;
+        if ((overlap || study) && partSize % slice == 0) {
+            for (int p = q.L - 1; p >= 0 && nRange < 3 && (nSlices >> (nRange + 1)) >= 1; p--) {
+                bool swapped = false;
+                for (int m = 0; m < k; m++) swapped = swapped || lpos[m] == p;
+                if (!swapped) rangePos[nRange++] = p;
+            }
+            if (nRange) {
+                // (ascending: bit m of a range index is rangePos[m], the top
+                // nRange bits of the packed part index)
+                std::reverse(rangePos, rangePos + nRange);
+                perRange = nSlices >> nRange;
+                be::swapRanges(q, rangePos, nRange);
+                // the first pass after the swap holds the incoming qubits: it
+                // keeps the ranges' positions out of its tile (their ops wait
+                // for the next pass), so it can run range by range
+                static const bool firstAvoid = !getenv("QUEST_SWAP_RANGES_FIRST") || atoi(getenv("QUEST_SWAP_RANGES_FIRST")) != 0;
+                if (firstAvoid)
+                    for (int i = 0; i < nRange; i++) q.firstPassAvoid |= 1ull << rangePos[i];
+                if (!overlap) nRange = 0;   // (study: no range events)
+            }
+        }
         auto unpack = [&](i64 s) {
             const int b = (int)(s & 1);
             const i64 off = s * slice, n = std::min(slice, partSize - off);
@@ -336,6 +367,7 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn0, int k) {
                 real* r = g_x.recv[(size_t)(b * np + d - 1)];
                 be::unpackBits(q, lpos, k, setMask[myG ^ d], off, n, r, r + n);
             }
+            if (nRange && (s + 1) % perRange == 0) be::swapRangeLanded(q, (int)(s / perRange));
         };
         for (i64 s = 0; s < nSlices; s++) {
             const int b = (int)(s & 1);

@@ -607,9 +607,11 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
     if (commute)
         for (int i = 0; i < n; i++) cls[i] = (unsigned char)commuteClass(ops[i]);
     // one greedy scan from `first` with the high bits `preset` claimed up front
+    const u64 firstAvoid = hooks ? hooks->firstPassAvoid : 0;
     auto scan = [&](u64 preset, std::vector<int>& picked) {
         picked.clear();
         u64 high = preset;
+        const u64 hardAvoid = out.passes.empty() ? firstAvoid : 0;
         u64 blockedTg = 0;      // targets of ops deferred past this pass
         u64 blockedTouch = 0;   // targets | controls of deferred ops
         // (class-aware) deferred targets of diagonal / X-class / general ops,
@@ -628,7 +630,8 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 free = !(tg & blockedTouch) && !(touch & blockedTg);
             }
             const u64 need = high | (tg & ~low);
-            if (free && popcount64(need) <= highSlots && (maxOps <= 0 || (int)picked.size() < maxOps)) {
+            if (free && !(tg & hardAvoid) && popcount64(need) <= highSlots &&
+                (maxOps <= 0 || (int)picked.size() < maxOps)) {
                 high = need;
                 picked.push_back(i);
             } else {
@@ -788,7 +791,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         for (int i = first; i < n && seeds < maxSeeds; i++) {
             if (done[i]) continue;
             const u64 h = targetMask(ops[i]) & ~low;
-            if (!h) continue;
+            if (!h || (out.passes.empty() && (h & firstAvoid))) continue;
             seeds++;
             bool dup = false;
             for (int t = 0; t < nTried; t++) dup |= tried[t] == h;
@@ -807,7 +810,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             order.push_back(ops[i]);
             done[i] = 1;
         }
-        emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out, avoid);
+        emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out, out.passes.empty() ? (avoid | firstAvoid) : avoid);
         if (relabelFrom >= 0 && (int)best.size() >= 2 && (int)order.size() < n) {
             // candidate store permutations (none, by first use, by use count),
             // each judged by how many ops the greedy plan of the NEXT pass

@@ -381,6 +381,8 @@ void swapMicrosReset() { g_swapUs = 0; }
 bool swapOverlapBegin(QuregImpl&, const int*, int, int) { return false; }
 void swapOverlapEnd(QuregImpl&) {}
 bool preSwap(QuregImpl&, const int*, int, int) { return false; }
+void swapRanges(QuregImpl&, const int*, int) {}
+void swapRangeLanded(QuregImpl&, int) {}
 
 u64 queuedTargets(const QuregImpl& q) {
     u64 m = 0xffull;   // the always-resident low positions of every wave tile (cmin <= 8)
@@ -498,6 +500,8 @@ void flushImpl(QuregImpl& q, bool front) {
     static const bool streamOn = !getenv("QUEST_PLAN_STREAM") || atoi(getenv("QUEST_PLAN_STREAM")) != 0;
     PlanHooks hooks;
     hooks.avoidMask = q.tileAvoid;
+    hooks.firstPassAvoid = q.firstPassAvoid;   // (router: a swap's receive ranges; QUEST_SWAP_RANGES_STUDY on this build)
+    q.firstPassAvoid = 0;
     hooks.relabelOk = [](const TilePass& ps, const TileOp* ops) { return waveLowers(ps, ops); };
     hooks.lowPerm = [](const TilePass& ps, const TileOp* ops, int c, int* sigma) {
         return waveLowPerm(ps, ops, c, sigma);

@@ -562,6 +562,90 @@ def test_overlapped_swaps_rccl_shared_gpu(genv, tmp_path, ranks):
     assert np.max(np.abs(a - b)) < 1e-10
 
 
+RANGES = r'''
+import json, sys
+import numpy as np
+import quest_amd as qa
+from quest_amd.models import random_layered
+from quest_amd.models.circuits import Circuit
+from quest_amd.ops import capi
+env = qa.Env()
+n = int(sys.argv[2])
+seeds = [int(x) for x in sys.argv[3].split(",")]
+rows, states = [], []
+for sd in seeds:
+    r = qa.Register(env, n)
+    r.init_plus()
+    capi.resetQuESTStats()
+    if sd < 0:
+        # crafted: layers on the low qubits, then the top (rank) qubit joins --
+        # its swap's first post-swap passes leave the high local positions
+        # out of their tiles, so they run range by range
+        rng = np.random.default_rng(-sd)
+        lo = n - 6
+        for layer in range(4):
+            for q in range(lo):
+                r.ry(q, float(rng.uniform(0, 3)))
+            for q in range(layer % 2, lo - 1, 2):
+                r.cnot(q, q + 1)
+        r.h(n - 1)
+        for layer in range(3):
+            for q in list(range(0, lo, 2)) + [n - 1]:
+                r.rx(q, float(rng.uniform(0, 3)))
+            r.cnot(n - 1, 0)
+    else:
+        random_layered(n, 20, seed=sd).apply(r)
+    r.sync()
+    st = capi.getQuESTStats()
+    rows.append({k: st[k] for k in ("swaps", "overlappedSwaps", "overlappedPasses")})
+    states.append(r.to_numpy())
+    r.close()
+if env.rank == 0:
+    np.save(sys.argv[1], np.array(states))
+    print("STATS " + json.dumps(rows))
+'''
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_swap_ranges_overlap_random_circuits_rccl_shared_gpu(genv, tmp_path, ranks):
+    """Receive-side swap overlap (round 6, be::swapRanges): RCCL ranks
+    sharing the GPU, exchange slices small enough that every swap has 8
+    ranges (QUEST_EXCHANGE_SLICE_KB).  A pass after a swap whose tile holds
+    the incoming qubit cannot wait on one part; when it leaves the high local
+    positions (the ranges' bits) out, it runs range by range as the ranges
+    land.  The first pass after such a swap keeps those positions out of its
+    tile (router: q.firstPassAvoid -- their ops wait for the next pass), so
+    every window, the crafted ones (-1, -2) and the bench seeds' 20-layer
+    random layered ones, overlaps at least one pass per swap; the states
+    equal the single-rank run's."""
+    from quest_amd.parallel import spawn_local
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    n = 22 + {2: 1, 4: 2}[ranks]
+    seeds = "-1,-2,7,11,12,13,17"
+    one, dist = str(tmp_path / "one.npy"), str(tmp_path / "dist.npy")
+    base = {"QUEST_BACKEND": "hip", "PYTHONPATH": os.path.dirname(here)}
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, "-c", RANGES, one, str(n), seeds], env=dict(os.environ, **base),
+                       capture_output=True, text=True, timeout=200)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    res = spawn_local(["-c", RANGES, dist, str(n), seeds], ranks,
+                      env_extra=dict(base, QUEST_COMM="rccl", QUEST_RCCL_SHARED_GPU="1", QUEST_COMM_TIMEOUT="150",
+                                     QUEST_EXCHANGE_SLICE_KB="512"), timeout=280)
+    for r, q in enumerate(res):
+        assert q.returncode == 0, f"rank {r}:\n{q.stdout[-1500:]}\n{q.stderr[-2500:]}"
+    rows = json.loads([ln for ln in res[0].stdout.splitlines() if ln.startswith("STATS")][0][6:])
+    print("per window (crafted x2, bench seeds):", rows)
+    for row in rows:
+        assert row["swaps"] >= 1 and row["overlappedSwaps"] >= 1, rows
+    for row in rows:
+        assert row["overlappedPasses"] >= row["overlappedSwaps"], rows
+    a, b = np.load(one), np.load(dist)
+    assert np.max(np.abs(a - b)) < 1e-10
+
+
 def test_fork_benchmark_30q_matches_host_build(genv, tmp_path):
     """The fork's 30-qubit benchmark program (examples/random_circuit_benchmark.c
     flow: 490 gates, then P(q_i=1) for all 30 qubits and 10 amplitudes) on the
