@@ -48,6 +48,8 @@ def test_bench_under_torchrun_ipc(ranks):
     assert d["config"]["swaps"] > 0, d["config"]     # rank qubits were swapped in
     assert d["config"]["norm_error"] < 1e-10
     assert d["value"] > 0 and d["steps"] == 4
+    # rank predicates are tags: every rank planned the same passes (round 6)
+    assert d["config"]["layout_aligns_max"] == 0, d["config"]
 
 
 @pytest.mark.parametrize("ranks", [2, 8])
@@ -76,3 +78,5 @@ def test_bench_under_torchrun_rccl_shared_gpu(ranks):
     assert "RCCL" in d["config"]["parallelism"]
     assert d["config"]["swaps"] > 0, d["config"]
     assert d["config"]["norm_error"] < 1e-10
+    assert d["config"]["layout_aligns_max"] == 0, d["config"]
+    assert all("overlapped_passes" in s for s in d["config"]["seeds"]), d["config"]["seeds"]
