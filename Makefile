@@ -44,12 +44,17 @@ INCLUDES   := -Iinclude -DQA_WAVE_SLOTS_F64=$(strip $(WAVE_SLOTS)) -DQA_WAVE_SLO
 CXXFLAGS   := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $(INCLUDES)
 HIPFLAGS   := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-function \
               -Wno-unused-result -munsafe-fp-atomics $(INCLUDES)
+# the Python binding's per-gate fast path (CPython C API, src/py/gatecall.c)
+PYTHON     ?= python3
+PY_INC     := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_paths()['include'])")
+PY_EXT     := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+GATECALL   := quest_amd/ops/_gatecall$(PY_EXT)
 HIPHOST    := -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $(INCLUDES) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 
 .PHONY: cpu hip all clean examples examples-hip asan-check
 
-cpu: $(LIBDIR)/libQuEST_cpu_f64.so $(LIBDIR)/libQuEST_cpu_f32.so $(LIBDIR)/libQuEST_cpu_f128.so
-hip: $(LIBDIR)/libQuEST_hip_f64.so $(LIBDIR)/libQuEST_hip_f32.so $(LIBDIR)/libQuEST.so
+cpu: $(LIBDIR)/libQuEST_cpu_f64.so $(LIBDIR)/libQuEST_cpu_f32.so $(LIBDIR)/libQuEST_cpu_f128.so $(GATECALL)
+hip: $(LIBDIR)/libQuEST_hip_f64.so $(LIBDIR)/libQuEST_hip_f32.so $(LIBDIR)/libQuEST.so $(GATECALL)
 all: cpu hip
 
 # ---------------------------------------------------------------- CPU build
@@ -67,6 +72,10 @@ $(eval $(call cpu_rules,1,32))
 # QuEST_PREC=4 (long double), host build only as in the reference
 # (QuEST/CMakeLists.txt:66-70 forbids it on the GPU)
 $(eval $(call cpu_rules,4,128))
+
+$(GATECALL): src/py/gatecall.c $(wildcard include/*.h)
+	gcc -O2 -fPIC -shared -std=c11 -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers \
+	    -Iinclude -I$(PY_INC) $< -o $@
 
 # ---------------------------------------------------------------- HIP build
 define hip_rules
@@ -138,4 +147,4 @@ asan-check: $(BUILD)/asan/api_stress
 	cd $(BUILD)/asan && ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1 ./api_stress
 
 clean:
-	rm -rf $(BUILD) $(LIBDIR)/*.so
+	rm -rf $(BUILD) $(LIBDIR)/*.so $(GATECALL)

@@ -51,21 +51,20 @@ class Circuit:
 
     # -- execution ---------------------------------------------------------
     def apply(self, reg):
-        """Apply to a quest_amd Register (one API call per gate)."""
+        """Apply to a quest_amd Register (one API call per gate; each gate
+        name's method is looked up once per call)."""
+        methods = {}
         for g in self.gates:
-            q = g.qubits
-            if g.param is None:
-                if g.name in ("cnot", "cy", "cz"):
-                    getattr(reg, g.name)(q[0], q[1])
-                elif g.name == "mcz":
-                    reg.mcz(list(q))
-                else:
-                    getattr(reg, g.name)(q[0])
+            name = g.name
+            f = methods.get(name)
+            if f is None:
+                f = methods[name] = getattr(reg, name)
+            if name == "mcz":
+                f(list(g.qubits))
+            elif g.param is None:
+                f(*g.qubits)
             else:
-                if g.name in ("crx", "cry", "crz", "cphase"):
-                    getattr(reg, g.name)(q[0], q[1], g.param)
-                else:
-                    getattr(reg, g.name)(q[0], g.param)
+                f(*g.qubits, g.param)
 
     def apply_oracle(self, o):
         """Apply to an oracle StateVector / DensityMatrix."""

@@ -13,6 +13,7 @@ terminating the interpreter (the library's error handler hook).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 
 import numpy as np
@@ -163,11 +164,15 @@ class _Binding:
         # wrappers test the plain counter `nerr` (cheap) before looking
         self._err = threading.local()
         self.nerr = 0
+        # the same count where the per-gate fast path (_gatecall) reads it
+        self._errflag = C.c_int(0)
+        self._gatecall = None
         HANDLER = C.CFUNCTYPE(None, C.c_int, C.c_char_p, C.c_char_p)
 
         def _handler(code, msg, func):
             self._err.value = (int(code), msg.decode(), func.decode())
             self.nerr += 1
+            self._errflag.value = self.nerr
 
         self._handler = HANDLER(_handler)  # keep alive
         self._null_handler = HANDLER()
@@ -215,7 +220,25 @@ class _Binding:
         if e is not None:
             self._err.value = None
             self.nerr -= 1
+            self._errflag.value = self.nerr
             raise QuESTError(*e)
+
+    def gatecall(self):
+        """The compiled per-gate fast path (src/py/gatecall.c) configured for
+        this library, or None (not built, or QUEST_PY_GATECALL=0): one- and
+        two-qubit gate methods of a Register call the C API without ctypes."""
+        if self._gatecall is None:
+            self._gatecall = False
+            if os.environ.get("QUEST_PY_GATECALL", "1") != "0":
+                try:
+                    from . import _gatecall as g
+                except ImportError:
+                    g = None
+                if g is not None and g.qureg_size() == C.sizeof(self.Qureg):
+                    addrs = [C.cast(self.fns[name], C.c_void_p).value for name in g.FUNCTIONS]
+                    g.configure(addrs, self.prec, C.addressof(self._errflag), self.check)
+                    self._gatecall = g
+        return self._gatecall or None
 
 
 _binding: _Binding | None = None

@@ -12,6 +12,10 @@ import numpy as np
 
 from . import capi
 
+# gate methods the compiled fast path provides (quest_amd/ops/_gatecall)
+_FAST_GATES = ("h", "x", "y", "z", "s", "t", "rx", "ry", "rz", "phase", "cnot", "cy", "cz", "crx", "cry", "crz",
+               "cphase")
+
 
 class Env:
     """``createQuESTEnv()`` wrapper; one per process (idempotent)."""
@@ -58,6 +62,14 @@ class Register:
         self.envobj = env
         self.q = (capi.createDensityQureg if density else capi.createQureg)(num_qubits, env.env)
         self._alive = True
+        self._fast = None
+        g = capi.binding().gatecall()
+        if g is not None:
+            # the gate methods below, bound to the compiled fast path (same C
+            # functions, validation and errors; src/py/gatecall.c)
+            self._fast = g.bind(C.addressof(self.q), C.sizeof(self.q))
+            for name in _FAST_GATES:
+                setattr(self, name, getattr(self._fast, name))
 
     # -- properties --------------------------------------------------------
     @property
@@ -74,6 +86,11 @@ class Register:
 
     def close(self):
         if self._alive:
+            if self._fast is not None:
+                self._fast.close()
+                for name in _FAST_GATES:
+                    self.__dict__.pop(name, None)
+                self._fast = None
             capi.destroyQureg(self.q, self.envobj.env)
             self._alive = False
 

@@ -31,6 +31,11 @@ struct State {
             else
                 out = fopen(e, "a");
             if (!out) out = stderr;
+            // the process clock's origin on CLOCK_MONOTONIC (Python's
+            // time.monotonic()), so host marks of a driver line up with "t"
+            const double mono = std::chrono::duration<double>(t0.time_since_epoch()).count();
+            fprintf(out, "{\"t\": 0, \"rank\": -1, \"ev\": \"trace_start\", \"monotonic\": %.6f}\n", mono);
+            fflush(out);
         }
         const char* r = getenv("QUEST_ROCTX");
         if (r && atoi(r) == 1) {

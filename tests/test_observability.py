@@ -21,7 +21,8 @@ def test_trace_events_distributed(tmp_path):
     evs = [json.loads(line) for line in trace.read_text().splitlines()]
     kinds = {e["ev"] for e in evs}
     assert {"create", "flush", "swap", "destroy"} <= kinds
-    assert {e["rank"] for e in evs} == {0, 1}
+    assert {e["rank"] for e in evs if e["ev"] != "trace_start"} == {0, 1}
+    assert all("monotonic" in e for e in evs if e["ev"] == "trace_start")
     flushes = [e for e in evs if e["ev"] == "flush"]
     assert all(e["ops_fused"] <= e["ops"] and e["passes"] >= 1 for e in flushes)
     swaps = [e for e in evs if e["ev"] == "swap"]
