@@ -756,6 +756,14 @@ int waveSearchMinQubits() {
     return v;
 }
 
+bool waveSearchSplitFirst(const QuregImpl& q) {
+    // (28 qubits, 10-layer windows of ~400 ops: the search held the window's
+    // first pass back by 1.2-2.2 ms, profiles/r6/search_split_ab.txt)
+    static const bool on = !getenv("QUEST_PLAN_SEARCH_SPLIT") || atoi(getenv("QUEST_PLAN_SEARCH_SPLIT")) != 0;
+    return on && waveSearchOn() && waveFrontSearch() && q.planStrategy < 0 && !q.strategySearch.valid() &&
+           q.L >= waveSearchMinQubits() && q.pending.size() > waveSearchMinOps() && !getenv("QUEST_WAVE_CMIN");
+}
+
 bool waveFrontSearch() {
     static const bool v = !getenv("QUEST_PLAN_SEARCH_FRONT") || atoi(getenv("QUEST_PLAN_SEARCH_FRONT")) != 0;
     return v;

@@ -242,6 +242,11 @@ int waveCostMinQubits();
 // has chosen one (default 0)
 bool waveFrontSearch();
 bool waveSearchOn();   // QUEST_PLAN_SEARCH (default 1)
+// A full flush of a queue the search would plan, with no front flush of the
+// window before it (the GPU is idle): launch the first pass at once (planned
+// as a front flush, the whole queue its lookahead) and search the rest while
+// it runs, instead of searching first (QUEST_PLAN_SEARCH_SPLIT, default 1).
+bool waveSearchSplitFirst(const QuregImpl& q);
 int waveFrontStrategy();
 // Plan (and lower) a flush with strategy idx (< 0: the default): sets the
 // hooks' knobs and *cmin, and the thread's conditional-frame switch until

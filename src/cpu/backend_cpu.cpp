@@ -468,6 +468,18 @@ namespace {
 void flushImpl(QuregImpl& q, bool front) {
     if (q.pending.empty()) return;
     const RankSkipScope rankScope(q);
+    // the window's first pass now, the strategy search over the rest while it
+    // runs (waveSearchSplitFirst); `searched` is then that search's choice for
+    // exactly the queue left
+    int searched = -1;
+    if (!front && waveSearchSplitFirst(q)) {
+        flushImpl(q, true);
+        if (q.pending.empty()) return;
+        if (q.strategySearch.valid()) {
+            searched = q.strategySearch.get();
+            q.planStrategy = searched;
+        }
+    }
     TileProgram prog;
     std::vector<Op> raw;
     if (rt().verify) raw = q.pending;
@@ -536,7 +548,7 @@ void flushImpl(QuregImpl& q, bool front) {
     if (searchable) {
         if (q.strategySearch.valid()) q.planStrategy = q.strategySearch.get();
         strategy = front ? (q.planStrategy >= 0 ? q.planStrategy : waveFrontStrategy())
-                         : searchWaveStrategy(q.pending, q.L, cminUse, hooks);
+                         : searched >= 0 ? searched : searchWaveStrategy(q.pending, q.L, cminUse, hooks);
     }
     const int cminBase = cminUse;
     WaveStrategyScope strategyScope(strategy, cminBase, hooks, &cminUse);

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--layers", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--seeds", default="7,11,12,13,17")
+    ap.add_argument("--marks", default=None, help="write the windows' CLOCK_MONOTONIC [start, queued, end] here "
+                    "(rocprofv3 kernel timestamps use the same clock: tools/experiments/window_busy.py)")
     args = ap.parse_args()
     path = os.environ.get("QUEST_TRACE")
     assert path and path not in ("1", "stderr"), "QUEST_TRACE=<file>"
@@ -50,6 +52,9 @@ def main():
         t2 = time.monotonic()
         marks.append((sd, t0, t1, t2))
     r.close()
+    if args.marks:
+        with open(args.marks, "w") as f:
+            json.dump([{"seed": sd, "start": t0, "queued": t1, "end": t2} for sd, t0, t1, t2 in marks], f)
     evs = [json.loads(line) for line in open(path)]
     mono = next(e["monotonic"] for e in evs if e["ev"] == "trace_start")
     for sd, t0, t1, t2 in marks:
