@@ -1,6 +1,9 @@
 #include "tiles.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <mutex>
 #include <cmath>
 #include <complex>
 #include <cstdlib>
@@ -547,8 +550,58 @@ void applyPerm(std::vector<Op>& ops, const std::vector<char>& done, int first, c
 
 }  // namespace
 
+namespace {
+// QUEST_PLAN_PROFILE=1: host time of planTiles by section, printed at exit
+// (where a small register's planning goes: tools/experiments/plan_profile.sh)
+struct PlanProfile {
+    static constexpr int N = 8;
+    const char* names[N] = {"prep", "candidates", "trim", "emit", "relabel-choice", "relabel-ok", "low-perm",
+                            "pass-ready"};
+    double ms[N] = {0};
+    long calls = 0, passes = 0;
+    std::mutex mu;
+    bool on = getenv("QUEST_PLAN_PROFILE") && atoi(getenv("QUEST_PLAN_PROFILE")) != 0;
+    ~PlanProfile() {
+        if (!on || !calls) return;
+        double tot = 0;
+        for (double x : ms) tot += x;
+        fprintf(stderr, "plan profile: %ld planTiles calls, %ld passes, %.3f ms (%.1f us / pass):", calls, passes, tot,
+                passes ? 1e3 * tot / passes : 0.0);
+        for (int i = 0; i < N; i++) fprintf(stderr, " %s %.3f", names[i], ms[i]);
+        fprintf(stderr, "\n");
+    }
+};
+PlanProfile& planProfile() {
+    static PlanProfile p;
+    return p;
+}
+struct PlanClock {
+    bool on;
+    double acc[PlanProfile::N] = {0};
+    std::chrono::steady_clock::time_point t;
+    PlanClock() : on(planProfile().on) {
+        if (on) t = std::chrono::steady_clock::now();
+    }
+    void lap(int k) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        acc[k] += std::chrono::duration<double, std::milli>(n - t).count();
+        t = n;
+    }
+    void flush(long passes) {
+        if (!on) return;
+        PlanProfile& p = planProfile();
+        std::lock_guard<std::mutex> g(p.mu);
+        for (int i = 0; i < PlanProfile::N; i++) p.ms[i] += acc[i];
+        p.calls++;
+        p.passes += passes;
+    }
+};
+}  // namespace
+
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom,
                const PlanHooks* hooks) {
+    PlanClock clk;
     out.passes.clear();
     out.ops.clear();
     out.perm.resize(L);
@@ -583,6 +636,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         n = (int)ops.size();
     }
 
+    clk.lap(0);
     // List scheduling with commutation: a pass greedily collects every queued
     // op whose targets fit the pass's tile bits and that commutes with all the
     // earlier ops left for later passes.  Two ops commute when neither's
@@ -805,12 +859,15 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 bestScore = sc;
             }
         }
+        clk.lap(1);
         if (hooks && hooks->passCost && hooks->memCost > 0 && best.size() > 1) trimPass(best, bestHigh);
+        clk.lap(2);
         for (int i : best) {
             order.push_back(ops[i]);
             done[i] = 1;
         }
         emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out, out.passes.empty() ? (avoid | firstAvoid) : avoid);
+        clk.lap(3);
         if (relabelFrom >= 0 && (int)best.size() >= 2 && (int)order.size() < n) {
             // candidate store permutations (none, by first use, by use count),
             // each judged by how many ops the greedy plan of the NEXT pass
@@ -869,11 +926,13 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                     }
                 }
             }
+            clk.lap(4);
             if (choice >= 0 && hooks && hooks->relabelOk) {
                 TilePass cand = ps;
                 for (int i = 0; i < cand.k; i++) cand.stPos[i] = pis[choice][cand.pos[i]];
                 if (!hooks->relabelOk(cand, out.ops.data() + cand.opBegin)) choice = -1;
             }
+            clk.lap(5);
             if (choice >= 0) {
                 const int* pi = pis[choice];
                 TilePass& last = out.passes.back();
@@ -892,7 +951,9 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 for (int x = 0; x < L; x++) out.perm[x] = sigma[out.perm[x]];
             }
         }
+        clk.lap(6);
         if (ready) hooks->passReady(out, (int)out.passes.size() - 1, order);
+        clk.lap(7);
         if (hooks && hooks->maxPasses > 0 && (int)out.passes.size() >= hooks->maxPasses && (int)order.size() < n) {
             if (hooks->leftover) {
                 hooks->leftover->clear();
@@ -903,6 +964,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         }
     }
     ops.swap(order);
+    clk.flush((long)out.passes.size());
 }
 
 namespace {

@@ -742,8 +742,12 @@ size_t waveSearchMinOps() {
 int waveCostMinQubits() {
     // compute-aware trimming costs a wave lowering per candidate pass: at 20
     // local qubits (passes of ~10 us) that host time outweighs what it saves
-    // (profiles/r4/search_small_registers.txt: 2.11 -> 1.79 us / gate without)
-    static const int v = getenv("QUEST_PLAN_COST_QUBITS") ? atoi(getenv("QUEST_PLAN_COST_QUBITS")) : 22;
+    // (profiles/r4/search_small_registers.txt: 2.11 -> 1.79 us / gate without).
+    // Round 6 (fused_sweep windows, profiles/r6/cost_qubits_ab.txt): below 30
+    // local qubits the passes it shortens are not memory-bound enough to pay
+    // for the passes it adds -- 22-26 qubits 1-30 % faster without it, 27 / 29
+    // neutral, 28 -2.8 % (22 before)
+    static const int v = getenv("QUEST_PLAN_COST_QUBITS") ? atoi(getenv("QUEST_PLAN_COST_QUBITS")) : 30;
     return v;
 }
 

@@ -615,14 +615,14 @@ def test_swap_ranges_overlap_random_circuits_rccl_shared_gpu(genv, tmp_path, ran
     positions (the ranges' bits) out, it runs range by range as the ranges
     land.  The first pass after such a swap keeps those positions out of its
     tile (router: q.firstPassAvoid -- their ops wait for the next pass), so
-    every window, the crafted ones (-1, -2) and the bench seeds' 20-layer
+    every window, the crafted ones (-1, -2) and two bench seeds' 20-layer
     random layered ones, overlaps at least one pass per swap; the states
     equal the single-rank run's."""
     from quest_amd.parallel import spawn_local
 
     here = os.path.dirname(os.path.abspath(__file__))
     n = 22 + {2: 1, 4: 2}[ranks]
-    seeds = "-1,-2,7,11,12,13,17"
+    seeds = os.environ.get("RANGES_SEEDS", "-1,-2,7,13")   # (all five bench seeds: profiles/r6/swap_ranges.txt)
     one, dist = str(tmp_path / "one.npy"), str(tmp_path / "dist.npy")
     base = {"QUEST_BACKEND": "hip", "PYTHONPATH": os.path.dirname(here)}
     import subprocess
