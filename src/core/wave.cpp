@@ -810,11 +810,16 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
             // workgroup overlaps compute and memory worst when they are close
             // (round 5: T = 1.2 sum max with C near M); QUEST_PLAN_SCORE_OVERLAP = alpha
             static const double alpha = getenv("QUEST_PLAN_SCORE_OVERLAP") ? atof(getenv("QUEST_PLAN_SCORE_OVERLAP")) : 0.0;
+            // QUEST_PLAN_SCORE_KNEE / _SLOPE (experiment): a pass costs M +
+            // slope * max(0, C - knee) instead of max(C, M) -- the hinge fitted
+            // to measured pass times (profiles/r6/pass_time_model.txt)
+            static const double knee = getenv("QUEST_PLAN_SCORE_KNEE") ? atof(getenv("QUEST_PLAN_SCORE_KNEE")) : 0.0;
+            static const double slope = getenv("QUEST_PLAN_SCORE_SLOPE") ? atof(getenv("QUEST_PLAN_SCORE_SLOPE")) : 1.0;
             double t = 0;
             for (const TilePass& ps : prog.passes) {
                 const double cyc = wavePassCycles(ps, prog.ops.data() + ps.opBegin);
                 const double c = cyc < 0 ? M : cyc;
-                t += std::max(c, M) + alpha * std::min(c, M);
+                t += knee > 0 ? M + slope * std::max(0.0, c - knee) : std::max(c, M) + alpha * std::min(c, M);
             }
             score[i] = t;
         }

@@ -576,6 +576,13 @@ void flushImpl(QuregImpl& q, bool front) {
     if (trace::on())
         trace::event("flush", "\"qubits\": %d, \"ops\": %zu, \"ops_fused\": %zu, \"passes\": %zu, \"plan_ms\": %.3f",
                      q.L, opsIn, q.pending.size(), prog.passes.size(), 1e3 * (trace::now() - tFlush0));
+    // QUEST_TRACE_PASS_CYCLES=1: each wave pass's modeled cycles (plan studies
+    // of the pass-time model, tools/experiments/score_study.py)
+    static const bool passCycles = getenv("QUEST_TRACE_PASS_CYCLES") != nullptr;
+    if (trace::on() && passCycles && wave)
+        for (const TilePass& ps : prog.passes)
+            trace::event("pass", "\"qubits\": %d, \"ops\": %d, \"engine\": \"plan\", \"wave_cycles\": %.0f", q.L,
+                         ps.opEnd - ps.opBegin, wavePassCycles(ps, prog.ops.data() + ps.opBegin));
     if (planner == 1)
         planPhases(prog, -1, regSlots());
     else if (planner == 2)

@@ -50,6 +50,11 @@ def join(args):
     rows = list(csv.DictReader(open(kfile)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     ks = [r for r in rows if any(g in r["Kernel_Name"] for g in GATE_KERNELS)]
+    # (the one-workgroup wave launch of the backend's start-up check has no
+    # pass event)
+    while len(ks) > len(passes) and "qa_wave_tile" in ks[0]["Kernel_Name"] and \
+            int(ks[0]["End_Timestamp"]) - int(ks[0]["Start_Timestamp"]) < 50000:
+        ks = ks[1:]
     if len(ks) != len(passes):
         print(f"warning: {len(ks)} gate kernels vs {len(passes)} pass events", file=sys.stderr)
     out = []
