@@ -90,10 +90,10 @@ def test_fuzz_without_rank_tags_plans_diverge(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport,ranks,seeds", [("ipc", 2, 30), ("rccl", 2, 10)])
+@pytest.mark.parametrize("transport,ranks,seeds", [("ipc", 2, 30), ("rccl", 2, 5)])
 def test_fuzz_programs_on_gpu(tmp_path, transport, ranks, seeds):
     """Fuzz programs on one GPU shared by 2 ranks: 30 with in-place IPC swaps,
-    10 through the production RCCL calls (QUEST_RCCL_SHARED_GPU=1: RCCL's
+    5 through the production RCCL calls (QUEST_RCCL_SHARED_GPU=1: RCCL's
     network transport over loopback, slow -- the programs swap every few
     ops), 22-qubit state vectors (21 local qubits: wave passes with
     relabelling), against the single-rank HIP run; every rank planned the
