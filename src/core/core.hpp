@@ -127,11 +127,12 @@ struct QuregImpl {
     // op does not apply here), tags handed out round robin
     std::vector<unsigned char> rankSkip;
     int rankTagNext = 0;
-    // local positions the first pass planned after a swap keeps out of its
-    // tile, targets included (router multiSwap: the swap's receive ranges,
-    // so that pass can run range by range as they land); consumed by the
-    // next flush that plans a pass
+    // local positions the first passes planned after a swap keep out of
+    // their tiles, targets included (router multiSwap: the swap's receive
+    // ranges, so those passes can run range by range as they land), and how
+    // many passes still do (consumed by the flushes that plan them)
     u64 firstPassAvoid = 0;
+    int firstAvoidLeft = 0;
     bool permIdentity() const {
         for (int i = 0; i < nSV; i++)
             if (l2p[i] != i) return false;
@@ -159,6 +160,17 @@ struct RankSkipScope {
     }
     ~RankSkipScope() { rankSkipTable() = prev; }
 };
+
+// A flush planned `passes` passes: the swap-range constraint holds for that
+// many fewer (QuregImpl::firstAvoidLeft)
+inline void consumeFirstAvoid(QuregImpl& q, int passes) {
+    if (q.firstAvoidLeft <= 0) return;
+    q.firstAvoidLeft -= passes;
+    if (q.firstAvoidLeft <= 0) {
+        q.firstAvoidLeft = 0;
+        q.firstPassAvoid = 0;
+    }
+}
 
 QuregImpl* impl(const Qureg& q);
 

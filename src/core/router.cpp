@@ -354,9 +354,17 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn0, int k) {
                 // the first pass after the swap holds the incoming qubits: it
                 // keeps the ranges' positions out of its tile (their ops wait
                 // for the next pass), so it can run range by range
-                static const bool firstAvoid = !getenv("QUEST_SWAP_RANGES_FIRST") || atoi(getenv("QUEST_SWAP_RANGES_FIRST")) != 0;
-                if (firstAvoid)
+                // (QUEST_SWAP_RANGES_FIRST: how many passes after the swap do,
+                // 0 none; the backend runs such passes range-major -- every one
+                // of them on range v as soon as v landed)
+                // (default 2: host plan study, 2 ranks x 28 local qubits, five
+                // bench seeds' windows: 64 passes with 1, 66 with 2, 69 with 3)
+                static const int firstAvoid = getenv("QUEST_SWAP_RANGES_FIRST") ? atoi(getenv("QUEST_SWAP_RANGES_FIRST"))
+                                                                                 : 2;
+                if (firstAvoid > 0) {
                     for (int i = 0; i < nRange; i++) q.firstPassAvoid |= 1ull << rangePos[i];
+                    q.firstAvoidLeft = firstAvoid;
+                }
                 if (!overlap) nRange = 0;   // (study: no range events)
             }
         }

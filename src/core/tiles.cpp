@@ -662,10 +662,11 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         for (int i = 0; i < n; i++) cls[i] = (unsigned char)commuteClass(ops[i]);
     // one greedy scan from `first` with the high bits `preset` claimed up front
     const u64 firstAvoid = hooks ? hooks->firstPassAvoid : 0;
+    const int firstAvoidN = hooks ? hooks->firstAvoidPasses : 0;
     auto scan = [&](u64 preset, std::vector<int>& picked) {
         picked.clear();
         u64 high = preset;
-        const u64 hardAvoid = out.passes.empty() ? firstAvoid : 0;
+        const u64 hardAvoid = (int)out.passes.size() < firstAvoidN ? firstAvoid : 0;
         u64 blockedTg = 0;      // targets of ops deferred past this pass
         u64 blockedTouch = 0;   // targets | controls of deferred ops
         // (class-aware) deferred targets of diagonal / X-class / general ops,
@@ -845,7 +846,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         for (int i = first; i < n && seeds < maxSeeds; i++) {
             if (done[i]) continue;
             const u64 h = targetMask(ops[i]) & ~low;
-            if (!h || (out.passes.empty() && (h & firstAvoid))) continue;
+            if (!h || ((int)out.passes.size() < firstAvoidN && (h & firstAvoid))) continue;
             seeds++;
             bool dup = false;
             for (int t = 0; t < nTried; t++) dup |= tried[t] == h;
@@ -866,7 +867,8 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             order.push_back(ops[i]);
             done[i] = 1;
         }
-        emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out, out.passes.empty() ? (avoid | firstAvoid) : avoid);
+        emitPass(order, begin, (int)order.size(), bestHigh, L, k, c, out,
+                 (int)out.passes.size() < firstAvoidN ? (avoid | firstAvoid) : avoid);
         clk.lap(3);
         if (relabelFrom >= 0 && (int)best.size() >= 2 && (int)order.size() < n) {
             // candidate store permutations (none, by first use, by use count),

@@ -190,9 +190,10 @@ struct PlanHooks {
     // 1: the greedy plan of the rest of the queue with first-use relabelling
     // counts the passes a candidate leaves) -- a strategy of the search
     int rollout = -1;
-    // positions the FIRST pass of this plan keeps out of its tile even as
-    // targets (ops targeting them wait for a later pass)
+    // positions the first `firstAvoidPasses` passes of this plan keep out of
+    // their tiles even as targets (ops targeting them wait for a later pass)
     u64 firstPassAvoid = 0;
+    int firstAvoidPasses = 1;
 };
 
 void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileProgram& out, int relabelFrom = -1,

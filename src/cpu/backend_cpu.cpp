@@ -513,7 +513,7 @@ void flushImpl(QuregImpl& q, bool front) {
     PlanHooks hooks;
     hooks.avoidMask = q.tileAvoid;
     hooks.firstPassAvoid = q.firstPassAvoid;   // (router: a swap's receive ranges; QUEST_SWAP_RANGES_STUDY on this build)
-    q.firstPassAvoid = 0;
+    hooks.firstAvoidPasses = q.firstAvoidLeft;
     hooks.relabelOk = [](const TilePass& ps, const TileOp* ops) { return waveLowers(ps, ops); };
     hooks.lowPerm = [](const TilePass& ps, const TileOp* ops, int c, int* sigma) {
         return waveLowPerm(ps, ops, c, sigma);
@@ -554,6 +554,7 @@ void flushImpl(QuregImpl& q, bool front) {
     WaveStrategyScope strategyScope(strategy, cminBase, hooks, &cminUse);
     planTiles(q.pending, q.L, wave ? kWaveBits : fuseQubits(), wave ? cminUse : 4, rt().fusion, prog,
               relabel ? kWaveVecBits : -1, relabel && streamOn ? &hooks : nullptr);
+    consumeFirstAvoid(q, (int)prog.passes.size());
     if (leftover.empty()) {   // the queue drained: choose afresh next time
         q.waveCmin = -1;
         q.planStrategy = -1;

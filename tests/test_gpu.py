@@ -613,7 +613,8 @@ def test_swap_ranges_overlap_random_circuits_rccl_shared_gpu(genv, tmp_path, ran
     ranges (QUEST_EXCHANGE_SLICE_KB).  A pass after a swap whose tile holds
     the incoming qubit cannot wait on one part; when it leaves the high local
     positions (the ranges' bits) out, it runs range by range as the ranges
-    land.  The first pass after such a swap keeps those positions out of its
+    land -- and the passes after it that do too run with it range-major (each
+    on range v as soon as v landed).  The first pass after such a swap keeps those positions out of its
     tile (router: q.firstPassAvoid -- their ops wait for the next pass), so
     every window, the crafted ones (-1, -2) and two bench seeds' 20-layer
     random layered ones, overlaps at least one pass per swap; the states
@@ -643,6 +644,11 @@ def test_swap_ranges_overlap_random_circuits_rccl_shared_gpu(genv, tmp_path, ran
         assert row["swaps"] >= 1 and row["overlappedSwaps"] >= 1, rows
     for row in rows:
         assert row["overlappedPasses"] >= row["overlappedSwaps"], rows
+    # the bench seeds' windows: the first two passes after the swap run as a
+    # range-major chain (QUEST_SWAP_RANGES_FIRST, default 2)
+    for sd, row in zip(seeds.split(","), rows):
+        if int(sd) >= 0:
+            assert row["overlappedPasses"] >= 2 * row["overlappedSwaps"], rows
     a, b = np.load(one), np.load(dist)
     assert np.max(np.abs(a - b)) < 1e-10
 
