@@ -9,7 +9,10 @@
  * (resolved by ctypes, passed here as addresses) to a per-register object
  * whose methods call them directly: same API functions, same validation and
  * error handler (an error sets `errflag`; the method then calls the Python
- * binding's check(), which raises QuESTError), the same QASM recording.
+ * binding's check(), which raises QuESTError), the same QASM recording.  As
+ * ctypes does, the call runs without the GIL (a gate can start a flush that
+ * waits for the GPU); the error handler is a ctypes callback, which takes the
+ * GIL itself.
  *
  * QuEST.h's Qureg holds only ints and pointers, so one layout serves every
  * precision; the angle argument's C type follows the loaded library's
@@ -85,14 +88,18 @@ static PyObject* done(void) {
 static PyObject* call1(Gates* g, PyObject* const* a, Py_ssize_t n, int f, const char* name) {
     int t;
     if (!ready(g, n, 1, name) || argInt(a[0], &t)) return NULL;
+    Py_BEGIN_ALLOW_THREADS
     ((Fn1)g_fn[f])(g->q, t);
+    Py_END_ALLOW_THREADS
     return done();
 }
 
 static PyObject* call2(Gates* g, PyObject* const* a, Py_ssize_t n, int f, const char* name) {
     int c, t;
     if (!ready(g, n, 2, name) || argInt(a[0], &c) || argInt(a[1], &t)) return NULL;
+    Py_BEGIN_ALLOW_THREADS
     ((Fn2)g_fn[f])(g->q, c, t);
+    Py_END_ALLOW_THREADS
     return done();
 }
 
@@ -101,12 +108,14 @@ static PyObject* call1a(Gates* g, PyObject* const* a, Py_ssize_t n, int f, const
     if (!ready(g, n, 2, name) || argInt(a[0], &t)) return NULL;
     const double x = PyFloat_AsDouble(a[1]);
     if (x == -1.0 && PyErr_Occurred()) return NULL;
+    Py_BEGIN_ALLOW_THREADS
     if (g_prec == 1)
         ((Fn1f)g_fn[f])(g->q, t, (float)x);
     else if (g_prec == 4)
         ((Fn1l)g_fn[f])(g->q, t, (long double)x);
     else
         ((Fn1d)g_fn[f])(g->q, t, x);
+    Py_END_ALLOW_THREADS
     return done();
 }
 
@@ -115,12 +124,14 @@ static PyObject* call2a(Gates* g, PyObject* const* a, Py_ssize_t n, int f, const
     if (!ready(g, n, 3, name) || argInt(a[0], &c) || argInt(a[1], &t)) return NULL;
     const double x = PyFloat_AsDouble(a[2]);
     if (x == -1.0 && PyErr_Occurred()) return NULL;
+    Py_BEGIN_ALLOW_THREADS
     if (g_prec == 1)
         ((Fn2f)g_fn[f])(g->q, c, t, (float)x);
     else if (g_prec == 4)
         ((Fn2l)g_fn[f])(g->q, c, t, (long double)x);
     else
         ((Fn2d)g_fn[f])(g->q, c, t, x);
+    Py_END_ALLOW_THREADS
     return done();
 }
 
