@@ -90,6 +90,37 @@ def test_34_qubits_circuit_then_inverse(genv):
     r.close()
 
 
+def test_search_split_window_then_inverse(genv):
+    """A 28-qubit, 10-layer window (~420 ops: below the front-flush
+    threshold, above the strategy search's): the full flush launches its first
+    pass at once and searches the rest while it runs (QUEST_PLAN_SEARCH_SPLIT,
+    wave.cpp waveSearchSplitFirst); U then U^dagger, each such a window, must
+    return |+...+> with every sampled amplitude 2^-14 to 1e-10."""
+    import quest_amd as qa
+    from quest_amd.models import random_layered
+
+    n = 28
+    u = random_layered(n, 10, seed=28)
+    assert 256 < len(u.gates) < 600
+    r = qa.Register(genv, n)
+    r.init_plus()
+    qa.capi.resetQuESTStats()
+    u.apply(r)
+    p_mid = r.prob(n // 2, 1)
+    assert 0 < p_mid < 1
+    u.inverse().apply(r)
+    r.sync()
+    st = qa.capi.getQuESTStats()
+    # two windows, each split into its first pass's flush and the rest
+    assert st["wavePasses"] > 0 and st["flushes"] >= 4, st
+    want = 2.0 ** (-n / 2)
+    for idx in (0, 1, 12345, (1 << n) - 1, 1 << 27, 987654321 % (1 << n)):
+        a = r.amp(idx)
+        assert abs(a - want) < 1e-10, (idx, a)
+    assert abs(r.total_prob() - 1) < 1e-10
+    r.close()
+
+
 def test_rccl_transport_self_test(genv):
     """The RCCL transport's own calls on hardware: a one-rank communicator
     runs the pipelined exchange (communication stream + events, 5 slices over
