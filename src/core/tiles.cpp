@@ -835,13 +835,20 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             return sc;
         };
         double bestScore = rollout ? -1e6 * rolloutPasses(best, bestHigh) + (double)best.size() : score(best);
+        // (48 seeds, 32 distinct target sets: round 6's host study priced by the
+        // measured pass-time model, profiles/r6/plan_seeds.txt -- 24 / 16 before)
         static const int maxSeedsEnv = [] {
             const char* e = getenv("QUEST_PLAN_SEEDS");
-            return e ? atoi(e) : 24;
+            return e ? atoi(e) : 48;
         }();
         const int maxSeeds = hooks && hooks->seeds > 0 ? hooks->seeds : maxSeedsEnv;
         int seeds = 0;
-        u64 tried[16];
+        // distinct seed target sets tried per pass (QUEST_PLAN_TRIED, at most 64)
+        static const int maxTried = [] {
+            const char* e = getenv("QUEST_PLAN_TRIED");
+            return e ? std::max(1, std::min(64, atoi(e))) : 32;
+        }();
+        u64 tried[64];
         int nTried = 0;
         for (int i = first; i < n && seeds < maxSeeds; i++) {
             if (done[i]) continue;
@@ -850,7 +857,7 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             seeds++;
             bool dup = false;
             for (int t = 0; t < nTried; t++) dup |= tried[t] == h;
-            if (dup || nTried == 16) continue;
+            if (dup || nTried == maxTried) continue;
             tried[nTried++] = h;
             const u64 hh = scan(h, take);
             const double sc = rollout ? -1e6 * rolloutPasses(take, hh) + (double)take.size() : score(take);

@@ -679,7 +679,7 @@ struct WaveStrategy {
 // environment as they are); the 8th is the round-3 planner (no compute-aware
 // passes, no conditional frame); then class-aware commutation variants
 const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1, -1}, {1, 1, 0, -1, 1, -1}, {0, 0, 0, -1, 1, -1},
-                                    {1, 0, 0, -1, 1, -1},   {0, 2, 0, -1, 1, -1},  {0, 1, 48, -1, 1, -1},
+                                    {1, 0, 0, -1, 1, -1},   {0, 2, 0, -1, 1, -1},  {0, 1, 96, -1, 1, -1},
                                     {0, 1, 0, 0.5, 1, -1},  {0, 0, 0, -1, 0, -1},  {0, -1, 0, -1, -1, 1},
                                     {1, 1, 0, -1, 1, 1},    {0, 0, 0, -1, 1, 1},   {1, 0, 0, -1, 1, 1},
                                     {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1},  {0, 1, 0, -1, 1, -1, 15000},

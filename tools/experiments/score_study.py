@@ -16,16 +16,37 @@ T0, K, KNEE = 5.812, 0.000345, 11500
 
 
 def main():
-    seeds = [int(s) for s in (sys.argv[1] if len(sys.argv) > 1 else "7,11,12,13,17").split(",")]
+    arg = sys.argv[1] if len(sys.argv) > 1 else "7,11,12,13,17"
+    if "-" in arg:
+        a, b = arg.split("-")
+        seeds = list(range(int(a), int(b) + 1))
+    else:
+        seeds = [int(s) for s in arg.split(",")]
     tot_p, tot_t = 0, 0.0
     out = []
+    procs = {}
+    par = int(os.environ.get("STUDY_JOBS", "4"))
+    pending = list(seeds)
+    traces = {}
+    while pending or procs:
+        while pending and len(procs) < par:
+            sd = pending.pop(0)
+            tr = f"/tmp/score_study_{os.getpid()}_{sd}.trace"
+            if os.path.exists(tr):
+                os.remove(tr)
+            env = dict(os.environ, QUEST_TRACE=tr, QUEST_TRACE_PASS_CYCLES="1")
+            procs[sd] = subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "plan_study.py"), "--seed",
+                                          str(sd)], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            traces[sd] = tr
+        for sd in list(procs):
+            if procs[sd].poll() is not None:
+                assert procs[sd].returncode == 0, sd
+                del procs[sd]
+        if procs:
+            import time
+            time.sleep(0.05)
     for sd in seeds:
-        tr = f"/tmp/score_study_{os.getpid()}_{sd}.trace"
-        if os.path.exists(tr):
-            os.remove(tr)
-        env = dict(os.environ, QUEST_TRACE=tr, QUEST_TRACE_PASS_CYCLES="1")
-        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "plan_study.py"), "--seed", str(sd)], env=env,
-                       check=True, capture_output=True)
+        tr = traces[sd]
         evs = [json.loads(line) for line in open(tr)]
         os.remove(tr)
         # the timed window: the passes after the warm-up's last flush (plan_study resets stats there)
