@@ -815,7 +815,9 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         int frontEnd = first;
         for (int c = 0; frontEnd < n && c < frontN; frontEnd++)
             if (!done[frontEnd]) c++;
-        static const double betaEnv = getenv("QUEST_PLAN_LOOKAHEAD") ? atof(getenv("QUEST_PLAN_LOOKAHEAD")) : 0.0;
+        // (0.3 since round 6 with the pass-time-model score of the search:
+        // profiles/r6/plan_seeds.txt; 0 before)
+        static const double betaEnv = getenv("QUEST_PLAN_LOOKAHEAD") ? atof(getenv("QUEST_PLAN_LOOKAHEAD")) : 0.3;
         const double beta = hooks && hooks->lookahead >= 0 ? hooks->lookahead : betaEnv;
         std::vector<int> nextTake;
         auto score = [&](const std::vector<int>& v) {

@@ -810,11 +810,12 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
             // workgroup overlaps compute and memory worst when they are close
             // (round 5: T = 1.2 sum max with C near M); QUEST_PLAN_SCORE_OVERLAP = alpha
             static const double alpha = getenv("QUEST_PLAN_SCORE_OVERLAP") ? atof(getenv("QUEST_PLAN_SCORE_OVERLAP")) : 0.0;
-            // QUEST_PLAN_SCORE_KNEE / _SLOPE (experiment): a pass costs M +
-            // slope * max(0, C - knee) instead of max(C, M) -- the hinge fitted
-            // to measured pass times (profiles/r6/pass_time_model.txt)
-            static const double knee = getenv("QUEST_PLAN_SCORE_KNEE") ? atof(getenv("QUEST_PLAN_SCORE_KNEE")) : 0.0;
-            static const double slope = getenv("QUEST_PLAN_SCORE_SLOPE") ? atof(getenv("QUEST_PLAN_SCORE_SLOPE")) : 1.0;
+            // a pass costs M + slope * max(0, C - knee): the hinge fitted to
+            // measured pass times (profiles/r6/pass_time_model.txt: 5.81 ms +
+            // 0.345 us per modeled cycle above 11500, i.e. 0.76 of M / 12800 per
+            // cycle); QUEST_PLAN_SCORE_KNEE=0: round 5's max(C, M)
+            static const double knee = getenv("QUEST_PLAN_SCORE_KNEE") ? atof(getenv("QUEST_PLAN_SCORE_KNEE")) : 11500.0;
+            static const double slope = getenv("QUEST_PLAN_SCORE_SLOPE") ? atof(getenv("QUEST_PLAN_SCORE_SLOPE")) : 0.76;
             double t = 0;
             for (const TilePass& ps : prog.passes) {
                 const double cyc = wavePassCycles(ps, prog.ops.data() + ps.opBegin);
