@@ -891,8 +891,9 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
                 size_t most = 0;
                 scan(0, pick);
                 most = pick.size();
+                static const int maxTries = getenv("QUEST_RELABEL_TRIES") ? atoi(getenv("QUEST_RELABEL_TRIES")) : 8;
                 int tries = 0;
-                for (int i = first; i < n && tries < 8; i++) {
+                for (int i = first; i < n && tries < maxTries; i++) {
                     if (done[i]) continue;
                     const u64 h = targetMask(ops[i]) & ~low;
                     if (!h) continue;

@@ -684,6 +684,9 @@ const WaveStrategy kStrategies[] = {{0, -1, 0, -1, -1, -1}, {1, 1, 0, -1, 1, -1}
                                     {1, 1, 0, -1, 1, 1},    {0, 0, 0, -1, 1, 1},   {1, 0, 0, -1, 1, 1},
                                     {-1, 1, 0, -1, 1, -1},  {-1, 0, 0, -1, 1, -1},  {0, 1, 0, -1, 1, -1, 15000},
                                     {0, 1, 0, -1, 1, -1, 17500},
+                                    // round 6: candidate lookahead off / strong (the default is 0.3)
+                                    {0, -1, 0, 0.0, -1, -1}, {0, 1, 0, 0.0, 1, -1}, {1, 1, 0, 0.0, 1, -1},
+                                    {0, 1, 0, 1.0, 1, -1},
                                     // round 6: rollout-scored candidates
                                     {0, 1, 0, -1, 1, -1, 0, 1}, {1, 1, 0, -1, 1, -1, 0, 2}, {0, 0, 0, -1, 1, -1, 0, 1},
                                     {0, 1, 0, -1, 1, -1, 0, 2}};
@@ -699,10 +702,11 @@ constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0])
 int searchStrategies() {
     static const int n = [] {
         const char* e = getenv("QUEST_PLAN_STRATEGIES");
-        // (round 6: the four rollout strategies after the first 16 are opt-in,
-        // QUEST_PLAN_STRATEGIES=20 -- bench seeds unchanged at 80 passes, fresh
-        // seeds 21-30 166 -> 163, at ten times the host time per strategy:
-        // profiles/r6/rollout_strategies.txt)
+        // (round 6: strategies 16-19, lookahead variants, and the four rollout
+        // ones after them are opt-in -- QUEST_PLAN_STRATEGIES=20: bench seeds
+        // 512 -> 502 predicted ms, fresh seeds 21-80 / 141-200 unchanged;
+        // =24: rollouts, fresh seeds 21-30 166 -> 163 passes at ten times the
+        // host time per strategy, profiles/r6/rollout_strategies.txt)
         const int v = e ? atoi(e) : 16;
         return v < 1 ? 1 : v > kNumStrategies ? kNumStrategies : v;
     }();
