@@ -90,7 +90,7 @@ def main():
     args = ap.parse_args()
     seeds = [args.seed] if args.seed is not None else [int(x) for x in args.seeds.split(",") if x]
 
-    from quest_amd.parallel import allreduce_max, barrier, init_distributed
+    from quest_amd.parallel import allreduce_max, barrier, init_distributed, shutdown
 
     rank, world = init_distributed()
     if world != args.gpus:
@@ -246,6 +246,7 @@ def main():
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
+    shutdown()
 
 
 def _median_time(fn, reps=5):

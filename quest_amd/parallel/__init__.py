@@ -73,6 +73,21 @@ def allreduce_max(x: float) -> float:
     return x
 
 
+def shutdown():
+    """End of a multi-rank job: every rank meets once more, then the
+    torch.distributed control plane goes down in order (a gloo process group
+    left to the interpreter's exit can abort a rank in its teardown --
+    "terminate called without an active exception")."""
+    try:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.barrier()
+            dist.destroy_process_group()
+    except ImportError:  # pragma: no cover
+        pass
+
+
 def spawn_local(script_args: list[str], nprocs: int, env_extra: dict | None = None, timeout: float = 300,
                 python: str | None = None):
     """Run ``python <script_args>`` as `nprocs` local ranks (used by the
