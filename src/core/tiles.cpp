@@ -817,7 +817,8 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
             if (!done[frontEnd]) c++;
         // (0.3 since round 6 with the pass-time-model score of the search:
         // profiles/r6/plan_seeds.txt; 0 before)
-        static const double betaEnv = getenv("QUEST_PLAN_LOOKAHEAD") ? atof(getenv("QUEST_PLAN_LOOKAHEAD")) : 0.3;
+        static const double betaEnv = getenv("QUEST_PLAN_LOOKAHEAD") ? atof(getenv("QUEST_PLAN_LOOKAHEAD"))
+                                                                       : (sizeof(real) == 8 ? 0.3 : 0.0);
         const double beta = hooks && hooks->lookahead >= 0 ? hooks->lookahead : betaEnv;
         std::vector<int> nextTake;
         auto score = [&](const std::vector<int>& v) {
@@ -841,14 +842,14 @@ void planTiles(std::vector<Op>& ops, int L, int kmax, int cmin, bool fuse, TileP
         // measured pass-time model, profiles/r6/plan_seeds.txt -- 24 / 16 before)
         static const int maxSeedsEnv = [] {
             const char* e = getenv("QUEST_PLAN_SEEDS");
-            return e ? atoi(e) : 48;
+            return e ? atoi(e) : (sizeof(real) == 8 ? 48 : 24);   // (fp32: not tuned with the model, round 5's)
         }();
         const int maxSeeds = hooks && hooks->seeds > 0 ? hooks->seeds : maxSeedsEnv;
         int seeds = 0;
         // distinct seed target sets tried per pass (QUEST_PLAN_TRIED, at most 64)
         static const int maxTried = [] {
             const char* e = getenv("QUEST_PLAN_TRIED");
-            return e ? std::max(1, std::min(64, atoi(e))) : 32;
+            return e ? std::max(1, std::min(64, atoi(e))) : (sizeof(real) == 8 ? 32 : 16);
         }();
         u64 tried[64];
         int nTried = 0;
