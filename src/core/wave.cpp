@@ -699,7 +699,11 @@ constexpr int kNumStrategies = (int)(sizeof kStrategies / sizeof kStrategies[0])
 // trimming against a larger memory budget, leave the bench seeds' plans as
 // they are and take fresh seeds 14-20 from 96 to 94 passes, 0.1247 -> 0.1233
 // ms / gate, profiles/r5/trim_budget_strategies_ab.txt)
-int searchStrategies() {
+int searchStrategies(int L) {
+    // from 30 local qubits (passes of 6 ms and more hide the longer search)
+    // the four lookahead variants join: host study, seeds 11-20 152 -> 150
+    // passes, the other seed sets -0.1 .. -2 % predicted (plan_seeds.txt)
+    if (!getenv("QUEST_PLAN_STRATEGIES")) return L >= 30 ? 20 : 16;
     static const int n = [] {
         const char* e = getenv("QUEST_PLAN_STRATEGIES");
         // (round 6: strategies 16-19, lookahead variants, and the four rollout
@@ -836,7 +840,7 @@ int searchWaveStrategy(const std::vector<Op>& ops, int L, int cdefault, const Pl
         took[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tRun0).count();
     };
     std::vector<std::thread> pool;
-    const int nStrat = searchStrategies();
+    const int nStrat = searchStrategies(L);
     const auto tSearch0 = std::chrono::steady_clock::now();
     for (int i = 1; i < nStrat; i++) pool.emplace_back(run, i);
     run(0);
