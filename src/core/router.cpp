@@ -357,10 +357,14 @@ void multiSwap(QuregImpl& q, const int* gposIn, const int* lposIn0, int k) {
                 // (QUEST_SWAP_RANGES_FIRST: how many passes after the swap do,
                 // 0 none; the backend runs such passes range-major -- every one
                 // of them on range v as soon as v landed)
-                // (default 2: host plan study, 2 ranks x 28 local qubits, five
-                // bench seeds' windows: 64 passes with 1, 66 with 2, 69 with 3)
-                static const int firstAvoid = getenv("QUEST_SWAP_RANGES_FIRST") ? atoi(getenv("QUEST_SWAP_RANGES_FIRST"))
-                                                                                 : 2;
+                // (default: 3 for swaps of 1 or 2 qubits, 2 for 3 -- a link
+                // carries 2^-k of the chunk, so the transfer hides fewer passes
+                // the larger k; host plan study, 2 ranks x 28 local qubits, five
+                // bench seeds' windows: 64 / 66 / 68 passes with 1 / 2 / 3
+                // chained, profiles/r6/range_chain.txt)
+                static const int firstAvoidEnv = getenv("QUEST_SWAP_RANGES_FIRST") ? atoi(getenv("QUEST_SWAP_RANGES_FIRST"))
+                                                                                    : -1;
+                const int firstAvoid = firstAvoidEnv >= 0 ? firstAvoidEnv : (k <= 2 ? 3 : 2);
                 if (firstAvoid > 0) {
                     for (int i = 0; i < nRange; i++) q.firstPassAvoid |= 1ull << rangePos[i];
                     q.firstAvoidLeft = firstAvoid;

@@ -644,11 +644,11 @@ def test_swap_ranges_overlap_random_circuits_rccl_shared_gpu(genv, tmp_path, ran
         assert row["swaps"] >= 1 and row["overlappedSwaps"] >= 1, rows
     for row in rows:
         assert row["overlappedPasses"] >= row["overlappedSwaps"], rows
-    # the bench seeds' windows: the first two passes after the swap run as a
-    # range-major chain (QUEST_SWAP_RANGES_FIRST, default 2)
+    # the bench seeds' windows: the first passes after the swap run as a
+    # range-major chain (QUEST_SWAP_RANGES_FIRST: 3 for swaps of 1-2 qubits)
     for sd, row in zip(seeds.split(","), rows):
         if int(sd) >= 0:
-            assert row["overlappedPasses"] >= 2 * row["overlappedSwaps"], rows
+            assert row["overlappedPasses"] >= 3 * row["overlappedSwaps"], rows
     a, b = np.load(one), np.load(dist)
     assert np.max(np.abs(a - b)) < 1e-10
 
